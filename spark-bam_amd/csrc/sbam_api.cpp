@@ -1,0 +1,780 @@
+// sbam_api.cpp — C-ABI (include/sbam.h) over the HIP kernels: device memory, stage orchestration,
+// Pos mapping, split assembly and error records.  Host code mirrors the reference's control flow:
+//   Channels / FindBlockStart / FindRecordStart / loadReadsAndPositions / loadSplitsAndReads
+//   (load/src/main/scala/org/hammerlab/bam/spark/load/CanLoadBam.scala:173-334),
+//   full-check Counts folding (cli/src/main/scala/org/hammerlab/bam/check/full/FullCheck.scala:141-191).
+#include "../../include/sbam.h"
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "sbam_internal.h"
+
+using namespace sbam;
+
+struct sbam_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int64_t D = 0, base = 0, file_size = 0;
+  uint8_t *d_comp = nullptr;
+  // candidates from the header scan
+  Candidate *d_cand = nullptr;
+  int64_t ncand = 0;
+  // block table (relative offsets), device + host
+  int64_t nblocks = -1;
+  int64_t *d_bstart = nullptr, *d_buoff = nullptr;
+  int32_t *d_bh = nullptr, *d_bc = nullptr, *d_bu = nullptr;
+  std::vector<int64_t> h_bstart, h_buoff;
+  std::vector<int32_t> h_bc, h_bu;
+  // uncompressed stream
+  uint8_t *d_u = nullptr;
+  int64_t L = -1;
+  // contig lengths
+  int32_t nref = -1;
+  int64_t *d_lens = nullptr;
+  std::vector<int64_t> h_lens;
+  sbam_pos header_end{0, 0, 0};
+  // success bitmap of the latest full/eager check
+  unsigned long long *d_bitmap = nullptr;
+  size_t bitmap_cap = 0;
+  int64_t bm_x0 = 0, bm_x1 = 0;
+  bool bm_valid = false;
+  int32_t bm_R = -1;
+  // inflate scratch
+  uint16_t *d_scratch = nullptr;
+  int nlanes = 0;
+  // small device scratch
+  int64_t *d_small = nullptr;  // 64 int64
+  unsigned long long *d_counts = nullptr;
+  // timing
+  std::map<std::string, std::pair<hipEvent_t, hipEvent_t>> ev;
+  sbam_error err{};
+};
+
+namespace {
+
+constexpr size_t kCountsWords = 21 * 19 + 21 + 21 * 128 + 19 * 19 + 4;
+
+int set_err(sbam_ctx *c, int code, const char *fmt, ...) {
+  c->err.code = code;
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(c->err.message, sizeof(c->err.message), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                     \
+  do {                                                                                        \
+    hipError_t e_ = (expr);                                                                   \
+    if (e_ != hipSuccess) return set_err(ctx, SBAM_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+hipError_t dalloc(T **p, size_t n) {
+  return hipMalloc(reinterpret_cast<void **>(p), std::max<size_t>(n, 1) * sizeof(T));
+}
+template <class T>
+void dfree(T *&p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+struct Timer {  // HIP events around a launch family on the ctx stream
+  sbam_ctx *c;
+  std::pair<hipEvent_t, hipEvent_t> *e;
+  Timer(sbam_ctx *c_, const char *name) : c(c_) {
+    auto it = c->ev.find(name);
+    if (it == c->ev.end()) {
+      std::pair<hipEvent_t, hipEvent_t> p;
+      (void)hipEventCreate(&p.first);
+      (void)hipEventCreate(&p.second);
+      it = c->ev.emplace(name, p).first;
+    }
+    e = &it->second;
+    (void)hipEventRecord(e->first, c->stream);
+  }
+  ~Timer() { (void)hipEventRecord(e->second, c->stream); }
+};
+
+StreamView view(sbam_ctx *c) {
+  return StreamView{c->d_u, c->L, c->d_lens, c->nref, (c->base + c->D >= c->file_size) ? 1 : 0};
+}
+
+// Header.make details at relative offset q (for HeaderParseException).
+int header_parse_error(sbam_ctx *c, int64_t q) {
+  uint8_t h[18] = {0};
+  const int64_t n = std::min<int64_t>(18, c->D - q);
+  if (n > 0) (void)hipMemcpy(h, c->d_comp + q, (size_t)n, hipMemcpyDeviceToHost);
+  static const int idxs[7] = {0, 1, 2, 3, 12, 13, 14};
+  static const int exps[7] = {31, 139, 8, 4, 66, 67, 2};
+  for (int j = 0; j < 7; j++)
+    if (h[idxs[j]] != (uint8_t)exps[j]) {
+      c->err.idx = idxs[j];
+      c->err.actual = (int8_t)h[idxs[j]];
+      c->err.expected = (int8_t)(uint8_t)exps[j];
+      c->err.position = c->base + q;
+      return set_err(c, SBAM_ERR_HEADER_PARSE, "Position %d: %d != %d", idxs[j], (int)(int8_t)h[idxs[j]],
+                     (int)(int8_t)(uint8_t)exps[j]);
+    }
+  return set_err(c, SBAM_ERR_HEADER_PARSE, "header parse failure at %lld", (long long)(c->base + q));
+}
+
+int ensure_blocks(sbam_ctx *c) {
+  if (c->nblocks < 0) return set_err(c, SBAM_ERR_STATE, "sbam_scan_blocks has not run");
+  return SBAM_OK;
+}
+int ensure_stream(sbam_ctx *c) {
+  if (c->L < 0) return set_err(c, SBAM_ERR_STATE, "sbam_inflate has not run");
+  if (c->nref < 0) return set_err(c, SBAM_ERR_STATE, "contig lengths unknown (sbam_header / sbam_set_contig_lengths)");
+  return SBAM_OK;
+}
+
+// block index whose (relative) start == q, or -1
+int64_t block_at(const sbam_ctx *c, int64_t q) {
+  auto it = std::lower_bound(c->h_bstart.begin(), c->h_bstart.end(), q);
+  if (it == c->h_bstart.end() || *it != q) return -1;
+  return it - c->h_bstart.begin();
+}
+// flat offset of Pos(end, 0) for relative compressed offset q: first block with start >= q
+int64_t x_end_of(const sbam_ctx *c, int64_t q) {
+  auto it = std::lower_bound(c->h_bstart.begin(), c->h_bstart.end(), q);
+  if (it == c->h_bstart.end()) return c->L;
+  return c->h_buoff[it - c->h_bstart.begin()];
+}
+sbam_pos pos_of(const sbam_ctx *c, int64_t x) {
+  // last block with uoff <= x and usize > 0 containing x; x at a block end normalises to (next, 0)
+  auto it = std::upper_bound(c->h_buoff.begin(), c->h_buoff.begin() + c->nblocks, x);
+  int64_t b = (it - c->h_buoff.begin()) - 1;
+  while (b >= 0 && b < c->nblocks && x >= c->h_buoff[b] + c->h_bu[b]) b++;
+  if (b < 0 || b >= c->nblocks) {
+    const int64_t endp = c->nblocks > 0 ? c->h_bstart[c->nblocks - 1] + c->h_bc[c->nblocks - 1] : 0;
+    return sbam_pos{c->base + endp, 0, 0};
+  }
+  return sbam_pos{c->base + c->h_bstart[b], (int32_t)(x - c->h_buoff[b]), 0};
+}
+
+int ensure_bitmap(sbam_ctx *c, int64_t x0, int64_t x1) {
+  const size_t words = (size_t)((x1 - x0 + 63) / 64) + 1;
+  if (words > c->bitmap_cap) {
+    dfree(c->d_bitmap);
+    HIPCHK(c, dalloc(&c->d_bitmap, words));
+    c->bitmap_cap = words;
+  }
+  return SBAM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *sbam_version(void) { return "sbam-mi355x 0.1 (gfx950)"; }
+
+int sbam_open(int device, const uint8_t *data, int64_t len, int64_t base_offset, int64_t file_size, sbam_ctx **out) {
+  if (!out || (!data && len > 0) || len < 0 || base_offset < 0 || file_size < base_offset + len) return SBAM_ERR_ARG;
+  sbam_ctx *c = new sbam_ctx();
+  *out = c;
+  c->device = device;
+  c->D = len;
+  c->base = base_offset;
+  c->file_size = file_size;
+  HIPCHK(c, hipSetDevice(device));
+  HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  HIPCHK(c, dalloc(&c->d_comp, (size_t)len + kCompPad));
+  HIPCHK(c, hipMemsetAsync(c->d_comp + len, 0, kCompPad, c->stream));
+  if (len) HIPCHK(c, hipMemcpyAsync(c->d_comp, data, (size_t)len, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, dalloc(&c->d_small, 64));
+  HIPCHK(c, dalloc(&c->d_counts, kCountsWords));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SBAM_OK;
+}
+
+void sbam_close(sbam_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  dfree(c->d_comp);
+  dfree(c->d_cand);
+  dfree(c->d_bstart);
+  dfree(c->d_buoff);
+  dfree(c->d_bh);
+  dfree(c->d_bc);
+  dfree(c->d_bu);
+  dfree(c->d_u);
+  dfree(c->d_lens);
+  dfree(c->d_bitmap);
+  dfree(c->d_scratch);
+  dfree(c->d_small);
+  dfree(c->d_counts);
+  for (auto &kv : c->ev) {
+    (void)hipEventDestroy(kv.second.first);
+    (void)hipEventDestroy(kv.second.second);
+  }
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const sbam_error *sbam_last_error(const sbam_ctx *c) { return c ? &c->err : nullptr; }
+
+double sbam_last_kernel_ms(sbam_ctx *c, const char *kernel) {
+  auto it = c->ev.find(kernel);
+  if (it == c->ev.end()) return -1.0;
+  (void)hipEventSynchronize(it->second.second);
+  float ms = -1.f;
+  if (hipEventElapsedTime(&ms, it->second.first, it->second.second) != hipSuccess) return -1.0;
+  return ms;
+}
+
+// ---- candidates (scan) ---------------------------------------------------------------------------
+static int scan_candidates(sbam_ctx *c) {
+  if (c->d_cand) return SBAM_OK;
+  Timer t(c, "scan");
+  const int64_t nchunks = (c->D + kScanChunk - 1) / kScanChunk;
+  int32_t *d_cc = nullptr;
+  int64_t *d_off = nullptr;
+  HIPCHK(c, dalloc(&d_cc, nchunks));
+  HIPCHK(c, dalloc(&d_off, nchunks));
+  HIPCHK(c, launch_scan_count(c->d_comp, c->D, d_cc, nchunks, c->stream));
+  HIPCHK(c, launch_scan_prefix(d_cc, nchunks, d_off, c->d_small, c->stream));
+  int64_t total = 0;
+  HIPCHK(c, hipMemcpyAsync(&total, c->d_small, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, dalloc(&c->d_cand, total));
+  c->ncand = total;
+  HIPCHK(c, launch_scan_write(c->d_comp, c->D, d_off, nchunks, c->d_cand, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  dfree(d_cc);
+  dfree(d_off);
+  return SBAM_OK;
+}
+
+int sbam_find_block_starts(sbam_ctx *c, const int64_t *starts, int64_t n, int32_t nchk, int64_t *out) {
+  if (!c || (!starts && n) || (!out && n) || nchk < 0) return SBAM_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = scan_candidates(c);
+  if (rc) return rc;
+  std::vector<int64_t> rel(n);
+  for (int64_t i = 0; i < n; i++) {
+    rel[i] = starts[i] - c->base;
+    if (rel[i] < 0 || rel[i] > c->D) return set_err(c, SBAM_ERR_ARG, "split start %lld outside loaded bytes", (long long)starts[i]);
+  }
+  int64_t *d_q = nullptr, *d_o = nullptr;
+  HIPCHK(c, dalloc(&d_q, n));
+  HIPCHK(c, dalloc(&d_o, n));
+  HIPCHK(c, hipMemcpyAsync(d_q, rel.data(), n * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, launch_find_block_starts(c->d_comp, c->D, c->d_cand, c->ncand, d_q, n, nchk, d_o, c->stream));
+  HIPCHK(c, hipMemcpyAsync(out, d_o, n * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  dfree(d_q);
+  dfree(d_o);
+  for (int64_t i = 0; i < n; i++) {
+    if (out[i] < 0) {
+      c->err.position = starts[i];
+      return set_err(c, SBAM_ERR_HEADER_SEARCH, "Failed to find a BGZF block header in %d bytes from %lld", 65536,
+                     (long long)starts[i]);
+    }
+    out[i] += c->base;
+  }
+  return SBAM_OK;
+}
+
+int sbam_scan_blocks(sbam_ctx *c, int64_t *n_blocks) {
+  if (!c) return SBAM_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = scan_candidates(c);
+  if (rc) return rc;
+  int64_t start_rel = 0;
+  if (c->base > 0) {  // a shard starts at the first block at/after its first byte
+    int64_t s = c->base, o = 0;
+    rc = sbam_find_block_starts(c, &s, 1, 5, &o);
+    if (rc) return rc;
+    start_rel = o - c->base;
+  }
+  Timer t(c, "chain");
+  std::vector<int64_t> st;
+  std::vector<int32_t> hs, cs, us;
+  int64_t first = 0;
+  HIPCHK(c, launch_lower_bound(c->d_cand, c->ncand, start_rel, c->d_small, c->stream));
+  HIPCHK(c, hipMemcpyAsync(&first, c->d_small, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  int64_t nb = 0;
+  bool fast = true;
+  if (start_rel + 18 > c->D) {
+    nb = 0;  // EOF before the first header: empty stream
+  } else {
+    Candidate c0{};
+    if (first < c->ncand) HIPCHK(c, hipMemcpy(&c0, c->d_cand + first, sizeof(Candidate), hipMemcpyDeviceToHost));
+    if (first >= c->ncand || c0.pos != start_rel) return header_parse_error(c, start_rel);
+    const unsigned long long none = ~0ull;
+    HIPCHK(c, hipMemcpyAsync(c->d_small + 1, &none, sizeof(none), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_chain_verify(c->d_cand, c->ncand, first, c->D, c->d_small + 1, c->stream));
+    unsigned long long stop = 0;
+    HIPCHK(c, hipMemcpyAsync(&stop, c->d_small + 1, sizeof(stop), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int64_t si = (int64_t)(stop >> 2);
+    const int code = (int)(stop & 3);
+    if (code == 1) nb = si - first;
+    else if (code == 2) nb = si - first + 1;
+    else fast = false;  // a candidate that is not the next header: walk exactly on the host
+  }
+  if (fast) {
+    HIPCHK(c, dalloc(&c->d_bstart, nb));
+    HIPCHK(c, dalloc(&c->d_bh, nb));
+    HIPCHK(c, dalloc(&c->d_bc, nb));
+    HIPCHK(c, dalloc(&c->d_bu, nb));
+    HIPCHK(c, launch_gather_blocks(c->d_cand, first, nb, c->d_bstart, c->d_bh, c->d_bc, c->d_bu, c->stream));
+    c->h_bstart.resize(nb);
+    c->h_bc.resize(nb);
+    c->h_bu.resize(nb);
+    HIPCHK(c, hipMemcpyAsync(c->h_bstart.data(), c->d_bstart, nb * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_bc.data(), c->d_bc, nb * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->h_bu.data(), c->d_bu, nb * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  } else {
+    std::vector<Candidate> hc(c->ncand);
+    HIPCHK(c, hipMemcpy(hc.data(), c->d_cand, c->ncand * sizeof(Candidate), hipMemcpyDeviceToHost));
+    int64_t q = start_rel, i = first;
+    std::vector<int32_t> h_h;
+    for (;;) {  // MetadataStream._advance, exactly (MetadataStream.scala:23-54)
+      if (q + 18 > c->D) break;
+      while (i < c->ncand && hc[i].pos < q) i++;
+      if (i >= c->ncand || hc[i].pos != q) return header_parse_error(c, q);
+      const Candidate &k = hc[i];
+      if (!(k.flags & CAND_ISIZE) || (k.flags & CAND_EMPTY)) break;
+      c->h_bstart.push_back(k.pos);
+      c->h_bc.push_back(k.csize);
+      c->h_bu.push_back(k.isize);
+      h_h.push_back(k.hsize);
+      q += k.csize;
+    }
+    nb = (int64_t)c->h_bstart.size();
+    HIPCHK(c, dalloc(&c->d_bstart, nb));
+    HIPCHK(c, dalloc(&c->d_bh, nb));
+    HIPCHK(c, dalloc(&c->d_bc, nb));
+    HIPCHK(c, dalloc(&c->d_bu, nb));
+    HIPCHK(c, hipMemcpy(c->d_bstart, c->h_bstart.data(), nb * 8, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_bh, h_h.data(), nb * 4, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_bc, c->h_bc.data(), nb * 4, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_bu, c->h_bu.data(), nb * 4, hipMemcpyHostToDevice));
+  }
+  c->h_buoff.resize(nb + 1);
+  int64_t acc = 0;
+  for (int64_t b = 0; b < nb; b++) {
+    c->h_buoff[b] = acc;
+    acc += (c->h_bu[b] < 0) ? 0 : c->h_bu[b];
+  }
+  c->h_buoff[nb] = acc;
+  HIPCHK(c, dalloc(&c->d_buoff, nb + 1));
+  HIPCHK(c, hipMemcpyAsync(c->d_buoff, c->h_buoff.data(), (nb + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->nblocks = nb;
+  if (n_blocks) *n_blocks = nb;
+  return SBAM_OK;
+}
+
+int sbam_get_blocks(sbam_ctx *c, int64_t *start, int32_t *csize, int32_t *usize, int64_t *uoff, int64_t cap) {
+  if (!c) return SBAM_ERR_ARG;
+  int rc = ensure_blocks(c);
+  if (rc) return rc;
+  if (cap < c->nblocks) return set_err(c, SBAM_ERR_ARG, "capacity %lld < %lld blocks", (long long)cap, (long long)c->nblocks);
+  for (int64_t b = 0; b < c->nblocks; b++) {
+    if (start) start[b] = c->base + c->h_bstart[b];
+    if (csize) csize[b] = c->h_bc[b];
+    if (usize) usize[b] = c->h_bu[b];
+    if (uoff) uoff[b] = c->h_buoff[b];
+  }
+  return SBAM_OK;
+}
+
+int sbam_inflate(sbam_ctx *c, int64_t *usz) {
+  if (!c) return SBAM_ERR_ARG;
+  int rc = ensure_blocks(c);
+  if (rc) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  const int64_t L = c->h_buoff[c->nblocks];
+  if (!c->d_u) {
+    HIPCHK(c, dalloc(&c->d_u, (size_t)L + kStreamPad));
+    HIPCHK(c, hipMemsetAsync(c->d_u + L, 0, kStreamPad, c->stream));
+  }
+  const int64_t nb = c->nblocks;
+  int lanes = (int)std::min<int64_t>(((nb + 255) / 256) * 256, 256LL * 256 * 2);  // ≤ 512 lanes per CU
+  if (lanes < 256) lanes = 256;
+  if (lanes > c->nlanes) {
+    dfree(c->d_scratch);
+    HIPCHK(c, dalloc(&c->d_scratch, (size_t)lanes * kInflateScratchU16));
+    c->nlanes = lanes;
+  }
+  int32_t *d_status = nullptr, *d_found = nullptr;
+  HIPCHK(c, dalloc(&d_status, nb));
+  HIPCHK(c, dalloc(&d_found, nb));
+  const unsigned long long none = ~0ull;
+  HIPCHK(c, hipMemcpyAsync(c->d_small + 2, &none, 8, hipMemcpyHostToDevice, c->stream));
+  BlockTable bt{c->d_bstart, c->d_bh, c->d_bc, c->d_bu, c->d_buoff, nb};
+  {
+    Timer t(c, "inflate");
+    HIPCHK(c, launch_inflate(c->d_comp, c->D, bt, c->d_u, c->d_scratch, lanes, d_status, d_found,
+                             reinterpret_cast<unsigned int *>(c->d_small + 3),
+                             reinterpret_cast<unsigned long long *>(c->d_small + 2), c->stream));
+  }
+  unsigned long long ferr = 0;
+  HIPCHK(c, hipMemcpyAsync(&ferr, c->d_small + 2, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (ferr != ~0ull) {
+    int32_t found = 0;
+    HIPCHK(c, hipMemcpy(&found, d_found + ferr, 4, hipMemcpyDeviceToHost));
+    c->err.position = c->base + c->h_bstart[ferr];
+    c->err.expected = c->h_bu[ferr];
+    c->err.actual = found;
+    dfree(d_status);
+    dfree(d_found);
+    return set_err(c, SBAM_ERR_INFLATE, "Expected %d decompressed bytes, found %d", c->h_bu[ferr], found);
+  }
+  dfree(d_status);
+  dfree(d_found);
+  c->L = L;
+  c->bm_valid = false;
+  if (usz) *usz = L;
+  return SBAM_OK;
+}
+
+int sbam_read_uncompressed(sbam_ctx *c, int64_t off, int64_t len, uint8_t *out) {
+  if (!c || off < 0 || len < 0) return SBAM_ERR_ARG;
+  if (c->L < 0) return set_err(c, SBAM_ERR_STATE, "sbam_inflate has not run");
+  if (off + len > c->L) return set_err(c, SBAM_ERR_ARG, "range past the stream end");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (len) HIPCHK(c, hipMemcpy(out, c->d_u + off, (size_t)len, hipMemcpyDeviceToHost));
+  return SBAM_OK;
+}
+
+int sbam_pos_to_offset(sbam_ctx *c, sbam_pos p, int64_t *off) {
+  if (!c || !off) return SBAM_ERR_ARG;
+  int rc = ensure_blocks(c);
+  if (rc) return rc;
+  const int64_t b = block_at(c, p.block_pos - c->base);
+  if (b < 0 || p.offset < 0 || p.offset > c->h_bu[b]) return set_err(c, SBAM_ERR_ARG, "no block at %lld", (long long)p.block_pos);
+  *off = c->h_buoff[b] + p.offset;
+  return SBAM_OK;
+}
+
+int sbam_offset_to_pos(sbam_ctx *c, int64_t off, sbam_pos *p) {
+  if (!c || !p) return SBAM_ERR_ARG;
+  int rc = ensure_blocks(c);
+  if (rc) return rc;
+  *p = pos_of(c, off);
+  return SBAM_OK;
+}
+
+// ---- BAM header -----------------------------------------------------------------------------------
+int sbam_set_contig_lengths(sbam_ctx *c, int32_t n_ref, const int64_t *lengths) {
+  if (!c || n_ref < 0 || (n_ref && !lengths)) return SBAM_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  dfree(c->d_lens);
+  HIPCHK(c, dalloc(&c->d_lens, n_ref));
+  if (n_ref) HIPCHK(c, hipMemcpy(c->d_lens, lengths, n_ref * 8, hipMemcpyHostToDevice));
+  c->h_lens.assign(lengths, lengths + n_ref);
+  c->nref = n_ref;
+  c->bm_valid = false;
+  return SBAM_OK;
+}
+
+int sbam_header(sbam_ctx *c, int32_t *n_ref, int64_t *lengths, int32_t cap, sbam_pos *end_pos) {
+  if (!c) return SBAM_ERR_ARG;
+  if (c->L < 0) return set_err(c, SBAM_ERR_STATE, "sbam_inflate has not run");
+  if (c->base != 0) return set_err(c, SBAM_ERR_STATE, "header lives in the file's first block (shard: sbam_set_contig_lengths)");
+  auto rd = [&](int64_t off, int64_t n, void *dst) -> bool {
+    if (off < 0 || off + n > c->L) return false;
+    return hipMemcpy(dst, c->d_u + off, (size_t)n, hipMemcpyDeviceToHost) == hipSuccess;
+  };
+  char magic[4];
+  if (!rd(0, 4, magic) || memcmp(magic, "BAM\1", 4) != 0)
+    return set_err(c, SBAM_ERR_NOT_BAM, "requirement failed");
+  int32_t l_text = 0, nr = 0;
+  if (!rd(4, 4, &l_text)) return set_err(c, SBAM_ERR_NOT_BAM, "truncated header");
+  int64_t x = 8 + (int64_t)l_text;
+  if (!rd(x, 4, &nr)) return set_err(c, SBAM_ERR_NOT_BAM, "truncated header");
+  x += 4;
+  std::vector<int64_t> lens;
+  for (int32_t i = 0; i < nr; i++) {
+    int32_t l_name = 0, l_ref = 0;
+    if (!rd(x, 4, &l_name)) return set_err(c, SBAM_ERR_NOT_BAM, "truncated header");
+    x += 4 + (int64_t)l_name;
+    if (!rd(x, 4, &l_ref)) return set_err(c, SBAM_ERR_NOT_BAM, "truncated header");
+    x += 4;
+    lens.push_back(l_ref);
+  }
+  int rc = sbam_set_contig_lengths(c, nr, lens.data());
+  if (rc) return rc;
+  c->header_end = pos_of(c, x);
+  if (n_ref) *n_ref = nr;
+  if (lengths)
+    for (int32_t i = 0; i < nr && i < cap; i++) lengths[i] = lens[i];
+  if (end_pos) *end_pos = c->header_end;
+  return SBAM_OK;
+}
+
+// ---- checkers ------------------------------------------------------------------------------------
+static int check_range_args(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R) {
+  int rc = ensure_stream(c);
+  if (rc) return rc;
+  if (x0 < 0 || x1 < x0 || x1 > c->L) return set_err(c, SBAM_ERR_ARG, "range [%lld, %lld) outside stream of %lld", (long long)x0, (long long)x1, (long long)c->L);
+  if (R < 0 || R > SBAM_MAX_READS_TO_CHECK) return set_err(c, SBAM_ERR_ARG, "reads_to_check %d out of range", R);
+  return SBAM_OK;
+}
+
+int sbam_check_eager(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, uint64_t *bitmap) {
+  if (!c) return SBAM_ERR_ARG;
+  int rc = check_range_args(c, x0, x1, R);
+  if (rc) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  rc = ensure_bitmap(c, x0, x1);
+  if (rc) return rc;
+  {
+    Timer t(c, "check_eager");
+    HIPCHK(c, launch_check_eager(view(c), x0, x1, R, c->d_bitmap, c->stream));
+  }
+  const size_t words = (size_t)((x1 - x0 + 63) / 64);
+  if (bitmap && words) HIPCHK(c, hipMemcpyAsync(bitmap, c->d_bitmap, words * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->bm_x0 = x0;
+  c->bm_x1 = x1;
+  c->bm_R = R;
+  c->bm_valid = true;
+  return SBAM_OK;
+}
+
+int sbam_check_full_words(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, uint32_t *words) {
+  if (!c || !words) return SBAM_ERR_ARG;
+  int rc = check_range_args(c, x0, x1, R);
+  if (rc) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  uint32_t *d_w = nullptr;
+  HIPCHK(c, dalloc(&d_w, x1 - x0));
+  {
+    Timer t(c, "check_words");
+    HIPCHK(c, launch_check_words(view(c), x0, x1, R, d_w, c->stream));
+  }
+  if (x1 > x0) HIPCHK(c, hipMemcpyAsync(words, d_w, (x1 - x0) * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  dfree(d_w);
+  return SBAM_OK;
+}
+
+int sbam_check_full_counts(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, sbam_counts *out, uint64_t *bitmap) {
+  if (!c || !out) return SBAM_ERR_ARG;
+  int rc = check_range_args(c, x0, x1, R);
+  if (rc) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  rc = ensure_bitmap(c, x0, x1);
+  if (rc) return rc;
+  HIPCHK(c, hipMemsetAsync(c->d_counts, 0, kCountsWords * 8, c->stream));
+  CountsDev cd;
+  cd.counts = c->d_counts;
+  cd.positions = cd.counts + 21 * 19;
+  cd.rbe = cd.positions + 21;
+  cd.pair = cd.rbe + 21 * 128;
+  cd.scalars = cd.pair + 19 * 19;
+  {
+    Timer t(c, "check_full");
+    HIPCHK(c, launch_check_full_counts(view(c), x0, x1, R, cd, c->d_bitmap, c->stream));
+  }
+  std::vector<unsigned long long> h(kCountsWords);
+  HIPCHK(c, hipMemcpyAsync(h.data(), c->d_counts, kCountsWords * 8, hipMemcpyDeviceToHost, c->stream));
+  const size_t words = (size_t)((x1 - x0 + 63) / 64);
+  if (bitmap && words) HIPCHK(c, hipMemcpyAsync(bitmap, c->d_bitmap, words * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  memset(out, 0, sizeof(*out));
+  const unsigned long long *p = h.data();
+  for (int k = 0; k < 21; k++)
+    for (int f = 0; f < 19; f++) out->counts[k][f] = (int64_t)p[k * 19 + f];
+  p += 21 * 19;
+  for (int k = 0; k < 21; k++) out->positions[k] = (int64_t)p[k];
+  p += 21;
+  for (int k = 0; k < 21; k++)
+    for (int r = 0; r < 128; r++) out->reads_before_error[k][r] = (int64_t)p[k * 128 + r];
+  p += 21 * 128;
+  for (int i = 0; i < 19; i++)
+    for (int j = 0; j < 19; j++) out->pair_hist[i][j] = (int64_t)p[i * 19 + j];
+  p += 19 * 19;
+  out->n_positions = x1 - x0;
+  out->n_success = (int64_t)p[1];
+  out->n_too_few_fixed = (int64_t)p[2];
+  out->n_halo = (int64_t)p[3];
+  c->bm_x0 = x0;
+  c->bm_x1 = x1;
+  c->bm_R = R;
+  c->bm_valid = true;
+  if (out->n_halo) {
+    c->err.actual = out->n_halo;
+    return set_err(c, SBAM_ERR_HALO, "%lld positions need bytes past the shard", (long long)out->n_halo);
+  }
+  return SBAM_OK;
+}
+
+static int find_record_starts(sbam_ctx *c, const std::vector<int64_t> &x0, int32_t R, int64_t mrs, bool use_bm,
+                              std::vector<int64_t> &out) {
+  const int64_t n = (int64_t)x0.size();
+  out.assign(n, -1);
+  if (!n) return SBAM_OK;
+  int64_t *d_x = nullptr, *d_o = nullptr;
+  HIPCHK(c, dalloc(&d_x, n));
+  HIPCHK(c, dalloc(&d_o, n));
+  HIPCHK(c, hipMemcpyAsync(d_x, x0.data(), n * 8, hipMemcpyHostToDevice, c->stream));
+  const bool bm = use_bm && c->bm_valid && c->bm_R == R;
+  {
+    Timer t(c, "find_record");
+    HIPCHK(c, launch_find_record_starts(view(c), d_x, n, R, mrs, bm ? c->d_bitmap : nullptr, c->bm_x0, c->bm_x1, d_o,
+                                        c->stream));
+  }
+  HIPCHK(c, hipMemcpyAsync(out.data(), d_o, n * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  dfree(d_x);
+  dfree(d_o);
+  return SBAM_OK;
+}
+
+int sbam_find_record_start(sbam_ctx *c, int64_t block_start, int32_t R, int32_t mrs, int32_t *found, sbam_pos *pos,
+                           int32_t *delta) {
+  if (!c || !found) return SBAM_ERR_ARG;
+  int rc = ensure_stream(c);
+  if (rc) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  *found = 0;
+  const int64_t b = block_at(c, block_start - c->base);
+  if (b < 0) return SBAM_OK;  // EOF-marker block / past the stream: the uncompressed stream is empty → None
+  std::vector<int64_t> x0{c->h_buoff[b]}, out;
+  rc = find_record_starts(c, x0, R, mrs, true, out);
+  if (rc) return rc;
+  if (out[0] == -2) return set_err(c, SBAM_ERR_HALO, "record search left the shard");
+  if (out[0] < 0) return SBAM_OK;
+  *found = 1;
+  if (pos) *pos = pos_of(c, out[0]);
+  if (delta) *delta = (int32_t)(out[0] - x0[0]);
+  return SBAM_OK;
+}
+
+// ---- splits ----------------------------------------------------------------------------------------
+int sbam_file_splits(int64_t file_size, int64_t split_size, int64_t *starts, int64_t *ends, int64_t cap, int64_t *n_out) {
+  if (split_size <= 0 || file_size < 0 || !n_out) return SBAM_ERR_ARG;
+  // FileInputFormat.getSplits: while (bytesRemaining / splitSize > SPLIT_SLOP) emit; then the remainder.
+  int64_t n = 0, off = 0, rem = file_size;
+  while ((double)rem / (double)split_size > 1.1) {
+    if (n < cap && starts) { starts[n] = off; ends[n] = off + split_size; }
+    n++;
+    off += split_size;
+    rem -= split_size;
+  }
+  if (rem > 0) {
+    if (n < cap && starts) { starts[n] = off; ends[n] = file_size; }
+    n++;
+  }
+  *n_out = n;
+  return SBAM_OK;
+}
+
+int sbam_split_records(sbam_ctx *c, const sbam_split_args *a, int64_t first, int64_t count, sbam_pos *first_pos,
+                       int32_t *found, int64_t *n_records) {
+  if (!c || !a || first < 0 || count < 0) return SBAM_ERR_ARG;
+  int rc = ensure_stream(c);
+  if (rc) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  int64_t ns = 0;
+  sbam_file_splits(c->file_size, a->split_size, nullptr, nullptr, 0, &ns);
+  if (first + count > ns) return set_err(c, SBAM_ERR_ARG, "split range past %lld splits", (long long)ns);
+  std::vector<int64_t> st(ns), en(ns);
+  sbam_file_splits(c->file_size, a->split_size, st.data(), en.data(), ns, &ns);
+  std::vector<int64_t> q(st.begin() + first, st.begin() + first + count), bs(count);
+  rc = sbam_find_block_starts(c, q.data(), count, a->bgzf_blocks_to_check, bs.data());
+  if (rc) return rc;
+  std::vector<int64_t> x0(count), xe(count);
+  for (int64_t i = 0; i < count; i++) {
+    const int64_t b = block_at(c, bs[i] - c->base);
+    if (b < 0) {  // FindRecordStart on the EOF marker: empty stream → None → NoReadFoundException
+      c->err.position = st[first + i];
+      return set_err(c, SBAM_ERR_NO_READ_FOUND, "Failed to find a valid read-start in %d attempts in %s from %lld",
+                     a->max_read_size, "path", (long long)bs[i]);
+    }
+    x0[i] = c->h_buoff[b];
+    xe[i] = x_end_of(c, en[first + i] - c->base);
+  }
+  std::vector<int64_t> xs;
+  rc = find_record_starts(c, x0, a->reads_to_check, a->max_read_size, a->use_success_bitmap != 0, xs);
+  if (rc) return rc;
+  for (int64_t i = 0; i < count; i++) {
+    if (xs[i] == -2) return set_err(c, SBAM_ERR_HALO, "record search left the shard");
+    if (xs[i] < 0) {
+      c->err.position = bs[i];
+      return set_err(c, SBAM_ERR_NO_READ_FOUND, "Failed to find a valid read-start in %d attempts in %s from %lld",
+                     a->max_read_size, "path", (long long)bs[i]);
+    }
+  }
+  int64_t *d_x = nullptr, *d_e = nullptr, *d_n = nullptr;
+  HIPCHK(c, dalloc(&d_x, count));
+  HIPCHK(c, dalloc(&d_e, count));
+  HIPCHK(c, dalloc(&d_n, count));
+  HIPCHK(c, hipMemcpyAsync(d_x, xs.data(), count * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_e, xe.data(), count * 8, hipMemcpyHostToDevice, c->stream));
+  {
+    Timer t(c, "records");
+    HIPCHK(c, launch_record_counts(view(c), d_x, d_e, count, d_n, c->stream));
+  }
+  std::vector<int64_t> cnt(count);
+  HIPCHK(c, hipMemcpyAsync(cnt.data(), d_n, count * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  dfree(d_x);
+  dfree(d_e);
+  dfree(d_n);
+  for (int64_t i = 0; i < count; i++) {
+    if (cnt[i] == -2) return set_err(c, SBAM_ERR_HALO, "record chain left the shard");
+    if (cnt[i] < 0) return set_err(c, SBAM_ERR_INFLATE, "UnexpectedEOF in record stream");
+    if (first_pos) first_pos[i] = pos_of(c, xs[i]);
+    if (found) found[i] = cnt[i] > 0;
+    if (n_records) n_records[i] = cnt[i];
+  }
+  return SBAM_OK;
+}
+
+int sbam_compute_splits(sbam_ctx *c, const sbam_split_args *a, sbam_split *splits, int64_t cap, int64_t *n_out) {
+  if (!c || !a || !n_out) return SBAM_ERR_ARG;
+  int64_t ns = 0;
+  sbam_file_splits(c->file_size, a->split_size, nullptr, nullptr, 0, &ns);
+  std::vector<sbam_pos> fp(ns);
+  std::vector<int32_t> fd(ns);
+  int rc = sbam_split_records(c, a, 0, ns, fp.data(), fd.data(), nullptr);
+  if (rc) return rc;
+  std::vector<sbam_pos> firsts;
+  for (int64_t i = 0; i < ns; i++)
+    if (fd[i]) firsts.push_back(fp[i]);
+  const int64_t n = (int64_t)firsts.size();
+  *n_out = n;
+  if (cap < n) return set_err(c, SBAM_ERR_ARG, "capacity %lld < %lld splits", (long long)cap, (long long)n);
+  for (int64_t i = 0; i < n; i++) {
+    splits[i].start = firsts[i];
+    splits[i].end = (i + 1 < n) ? firsts[i + 1] : sbam_pos{c->file_size, 0, 0};
+  }
+  return SBAM_OK;
+}
+
+int sbam_record_offsets(sbam_ctx *c, int64_t x0, int64_t x_end, int64_t *offsets, int64_t cap, int64_t *n_out) {
+  if (!c || !n_out || x0 < 0) return SBAM_ERR_ARG;
+  int rc = ensure_stream(c);
+  if (rc) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  int64_t *d_o = nullptr;
+  HIPCHK(c, dalloc(&d_o, cap));
+  HIPCHK(c, launch_record_offsets(view(c), x0, std::min(x_end, c->L), d_o, cap, c->d_small + 4, c->stream));
+  int64_t n = 0;
+  HIPCHK(c, hipMemcpyAsync(&n, c->d_small + 4, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (n < 0) n = -(n + 3);
+  if (offsets && n) HIPCHK(c, hipMemcpy(offsets, d_o, std::min(n, cap) * 8, hipMemcpyDeviceToHost));
+  dfree(d_o);
+  *n_out = n;
+  return SBAM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,80 @@
+// sbam_internal.h — launch wrappers shared by the kernels (sbam_kernels.hip) and the C-ABI host
+// layer (sbam_api.cpp).  Not part of the public ABI (include/sbam.h is).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sbam {
+
+// One BGZF header candidate found by the byte scan (Header.make, bgzf/.../block/Header.scala:48-83).
+struct Candidate {
+  int64_t pos;    // offset in the loaded buffer
+  int32_t hsize;  // 18 + XLEN - 6
+  int32_t csize;  // BSIZE + 1
+  int32_t isize;  // ISIZE (valid when flags & CAND_ISIZE)
+  int32_t flags;  // CAND_*
+};
+enum : int32_t { CAND_ISIZE = 1, CAND_EMPTY = 2 };
+
+// Device view of the BGZF block table (struct of arrays; offsets relative to the loaded buffer).
+struct BlockTable {
+  const int64_t *start;
+  const int32_t *hsize;
+  const int32_t *csize;
+  const int32_t *usize;
+  const int64_t *uoff;
+  int64_t n;
+};
+
+// Stream under check: uncompressed bytes u[0, L) (+ zero pad), contig lengths, EOF semantics.
+struct StreamView {
+  const uint8_t *u;
+  int64_t L;
+  const int64_t *lens;  // contig lengths (device)
+  int32_t nref;
+  int32_t eof_real;  // 1: L is the file's end; 0: a shard, reads past L are HALO
+};
+
+struct CountsDev {  // mirrors sbam_counts (int64 fields) in device memory
+  unsigned long long *counts;  // [21][19]
+  unsigned long long *positions;  // [21]
+  unsigned long long *rbe;  // [21][128]
+  unsigned long long *pair;  // [19][19]
+  unsigned long long *scalars;  // n_positions, n_success, n_too_few_fixed, n_halo
+};
+
+constexpr int kScanChunk = 1 << 20;  // bytes per workgroup in the BGZF candidate scan
+constexpr int kInflateScratchU16 = 2048;  // per-lane Huffman table scratch (u16 entries)
+constexpr int kStreamPad = 16384;  // zero pad behind the uncompressed stream (>= checker LDS window)
+constexpr int kCompPad = 64;  // zero pad behind the compressed bytes (bit-reader lookahead)
+
+hipError_t launch_scan_count(const uint8_t *d, int64_t D, int32_t *chunk_counts, int64_t nchunks, hipStream_t s);
+hipError_t launch_scan_prefix(int32_t *chunk_counts, int64_t nchunks, int64_t *chunk_offsets, int64_t *total,
+                              hipStream_t s);
+hipError_t launch_scan_write(const uint8_t *d, int64_t D, const int64_t *chunk_offsets, int64_t nchunks,
+                             Candidate *cands, hipStream_t s);
+hipError_t launch_chain_verify(const Candidate *cands, int64_t ncand, int64_t first, int64_t D, int64_t *first_stop,
+                               hipStream_t s);
+hipError_t launch_find_block_starts(const uint8_t *d, int64_t D, const Candidate *cands, int64_t ncand,
+                                    const int64_t *starts, int64_t n, int32_t blocks_to_check, int64_t *out,
+                                    hipStream_t s);
+hipError_t launch_gather_blocks(const Candidate *cands, int64_t first, int64_t n, int64_t *start, int32_t *hsize,
+                                int32_t *csize, int32_t *usize, hipStream_t s);
+hipError_t launch_inflate(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *out, uint16_t *scratch, int nlanes,
+                          int32_t *status, int32_t *found, unsigned int *next_block, unsigned long long *first_err,
+                          hipStream_t s);
+hipError_t launch_lower_bound(const Candidate *c, int64_t n, int64_t q, int64_t *out, hipStream_t s);
+hipError_t launch_check_full_counts(StreamView sv, int64_t x0, int64_t x1, int32_t R, CountsDev cd,
+                                    unsigned long long *bitmap, hipStream_t s);
+hipError_t launch_check_eager(StreamView sv, int64_t x0, int64_t x1, int32_t R, unsigned long long *bitmap,
+                              hipStream_t s);
+hipError_t launch_check_words(StreamView sv, int64_t x0, int64_t x1, int32_t R, uint32_t *words, hipStream_t s);
+hipError_t launch_find_record_starts(StreamView sv, const int64_t *x0, int64_t n, int32_t R, int64_t max_read_size,
+                                     const unsigned long long *bitmap, int64_t bitmap_x0, int64_t bitmap_x1,
+                                     int64_t *out, hipStream_t s);
+hipError_t launch_record_counts(StreamView sv, const int64_t *x0, const int64_t *x_end, int64_t n, int64_t *counts,
+                                hipStream_t s);
+hipError_t launch_record_offsets(StreamView sv, int64_t x0, int64_t x_end, int64_t *offsets, int64_t cap,
+                                 int64_t *n_out, hipStream_t s);
+
+}  // namespace sbam

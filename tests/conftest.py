@@ -1,0 +1,51 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(ROOT, "oracle"), os.path.join(ROOT, "spark-bam_amd"), ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+FIXTURES = os.path.join(ROOT, "tests", "fixtures")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+# The reference's record-indexed test BAMs (test_bams/src/main/resources, cli/src/test/resources/slice)
+INDEXED_BAMS = ["1.bam", "2.bam", "5k.bam", "1.2203053-2211029.bam", "2.100-1000.bam"]
+ALL_BAMS = INDEXED_BAMS + ["1.block-aligned.bam"]
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libsbam.so)")
+
+
+def fixture_bytes(name):
+    with open(os.path.join(FIXTURES, name), "rb") as f:
+        return f.read()
+
+
+@pytest.fixture(scope="session")
+def oracle_files():
+    import oracle
+    cache = {}
+
+    def get(name):
+        if name not in cache:
+            cache[name] = oracle.BamFile(fixture_bytes(name))
+        return cache[name]
+    return get
+
+
+@pytest.fixture(scope="session")
+def gpu_files():
+    import sbam
+    cache = {}
+
+    def get(name):
+        if name not in cache:
+            cache[name] = sbam.BamFile(fixture_bytes(name), path=name)
+        return cache[name]
+    yield get
+    for f in cache.values():
+        f.close()
