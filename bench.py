@@ -1,0 +1,205 @@
+#!/usr/bin/env python3
+"""bench.py — compressed-BAM GB/s for compute-splits + full-check on MI355X (BASELINE.json `metric`).
+
+Workload (configs[1]/[2] of BASELINE.json): a synthetic Illumina-like BAM (150 bp paired
+reads, zlib level 6, htsjdk-style 65498-B payloads, records straddling blocks; tools/synth_bam.c) of
+--size-gb compressed bytes PER GPU.  One step = the whole hot path over the whole file from compressed bytes
+resident in HBM:
+
+    BGZF header scan → block chain → inflate every block → full checker at every uncompressed offset
+    (Counts + success bitmap) → per Hadoop split (2 MiB): FindBlockStart → FindRecordStart → record chain
+    → split assembly (+ all_gather of split starts / all_reduce of Counts when N > 1)
+
+N > 1: one process per GPU (torch.distributed, RCCL), rank r owns a contiguous run of Hadoop splits of an
+N × size-gb file (weak scaling) and loads only its byte range + halo (sbam/dist.py).
+
+Prints ONE JSON line (rank 0).  `roofline` is for the dominant kernel (largest average device time),
+measured with HIP events on the library's stream over the timed steps; `cpu_baseline` times the CPU oracle
+(oracle/, a C restatement of the reference — the Scala/Spark reference cannot run on this image) on a
+bounded sample of the same generator on the host cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(ROOT, "spark-bam_amd"), os.path.join(ROOT, "tools")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(sample_mb: float, threads: int, split_size: int, seed: int):
+    """Oracle (C restatement of the reference algorithm) on a bounded sample of the same synthetic stream:
+    zlib inflate + full checker at every position + compute-splits, `threads` host threads."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    import synth
+    s = synth.SynthBam(tile_mb=sample_mb, copies=1, seed=seed, threads=threads)
+    data = s.bytes()
+    t0 = time.perf_counter()
+    f = oracle.BamFile(data, threads=threads)
+    _, _, _, nsucc = f.counts_parallel(0, f.L, 10, threads)
+    splits, parts = oracle.compute_splits(f, split_size)
+    wall = time.perf_counter() - t0
+    assert nsucc == s.n_records and sum(len(p) for p in parts) == s.n_records, "oracle sample self-check failed"
+    return {"value": round(data.size / wall / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"{data.size / 1e6:.1f} MB compressed ({f.L / 1e6:.1f} MB uncompressed, {s.n_records} records) "
+                      f"of the same synthetic generator: zlib inflate + full check of every offset + "
+                      f"compute-splits @ {split_size >> 20} MiB, {wall:.2f} s wall"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--size-gb", type=float, default=10.0, help="compressed GB per GPU")
+    ap.add_argument("--split-mb", type=float, default=2.0)
+    ap.add_argument("--tile-mb", type=float, default=64.0)
+    ap.add_argument("--threads", type=int, default=16, help="host threads (generator, CPU baseline)")
+    ap.add_argument("--cpu-sample-mb", type=float, default=64.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EEDBA11)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    import torch
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist = None
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import sbam
+    import synth
+    from sbam import dist as sdist
+
+    split_size = int(args.split_mb * (1 << 20))
+    t = time.time()
+    s = synth.SynthBam.for_size(int(args.size_gb * 1e9 * world), tile_mb=args.tile_mb, seed=args.seed,
+                                threads=args.threads)
+    plans = sdist.plan_shards(s.size, split_size, world)
+    plan = plans[rank]
+    shard = sdist.GpuShard(plan, s.slice, split_size, s.contig_lengths, device=local)
+    log(f"[rank {rank}] synthetic file {s.size / 1e9:.2f} GB ({s.n_records} records), shard "
+        f"[{plan.lo}, {plan.owned_hi}) splits {plan.split_first}+{plan.split_count}, setup {time.time() - t:.1f}s")
+
+    def step():
+        res = shard.step()
+        if world > 1:
+            sdist.gather_results(res, plans, device=dev)
+        return res
+
+    def sync():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+
+    res = None
+    for _ in range(args.warmup):
+        res = step()
+    kernels = ("scan", "chain", "inflate", "check_full", "find_record", "records")
+    tot_ms = {k: 0.0 for k in kernels}
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+        for k in kernels:
+            ms = shard.f.kernel_ms(k)
+            tot_ms[k] += max(ms, 0.0)
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    # --- size-independent parity properties of the last step (full sizes; fixtures cover exactness)
+    f = shard.f
+    counts = sdist.unpack_counts(res.counts)
+    n_rec = int(res.n_records.sum())
+    ok_local = counts["n_success"] == int(res.n_records.sum()) if world == 1 else True
+    if world > 1:
+        v = torch.tensor([counts["n_success"], n_rec], dtype=torch.int64, device=dev)
+        dist.all_reduce(v)
+        tot_succ, tot_rec = (int(x) for x in v.tolist())
+    else:
+        tot_succ, tot_rec = counts["n_success"], n_rec
+    parity = {"records": tot_rec, "expected_records": s.n_records, "checker_true": tot_succ,
+              "ok": bool(tot_rec == s.n_records and tot_succ == s.n_records and ok_local)}
+    if not parity["ok"]:
+        log(f"[rank {rank}] PARITY PROPERTY FAILED: {parity}")
+
+    # --- roofline of the dominant kernel (this rank's shard; per launch)
+    st, cs, us, uo = f.blocks()
+    comp_payload = int(cs.astype(np.int64).sum())
+    U = int(f.uncompressed_size)
+    avg = {k: tot_ms[k] / args.steps for k in kernels}
+    alg = {"inflate": comp_payload + U, "check_full": U + U // 8,
+           "scan": 2 * int(f._buf.size), "records": 0, "find_record": 0, "chain": 0}
+    dom = max(("inflate", "check_full", "scan"), key=lambda k: avg[k])
+    achieved = alg[dom] / (avg[dom] * 1e-3) / 1e9 if avg[dom] > 0 else 0.0
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                cpu = cpu_baseline(args.cpu_sample_mb, args.threads, split_size, args.seed)
+            except Exception as e:  # reported, never substituted for the GPU number
+                log(f"cpu baseline failed: {e!r}")
+        value = s.size * args.steps / elapsed / 1e9
+        line = {
+            "metric": "compressed BAM GB/s for compute-splits + full-check (whole node, 1/2/4/8 GPU)",
+            "value": round(value, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (tools/synth_bam.c: 150bp paired Illumina-like, zlib-6 BGZF, seed %#x)" % args.seed,
+            "config": {"workload": "Synthetic %.0f GB Illumina-like BAM per GPU: compute-splits @ %g MiB + "
+                                   "full-check of every uncompressed offset" % (args.size_gb, args.split_mb),
+                       "file_gb": round(s.size / 1e9, 3), "uncompressed_gb_per_gpu": round(U / 1e9, 3),
+                       "records": s.n_records, "blocks_per_gpu": int(st.size), "split_mb": args.split_mb,
+                       "parallelism": f"shard{world}"},
+            "uncompressed_gbps": round(U * world * args.steps / elapsed / 1e9, 3),
+            "kernel_ms": {k: round(v, 3) for k, v in avg.items()},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "algorithmic_bytes": alg[dom]},
+            "checker_roofline": {"achieved": round(alg["check_full"] / (avg["check_full"] * 1e-3) / 1e9, 2)
+                                 if avg["check_full"] > 0 else None,
+                                 "frac": round(alg["check_full"] / (avg["check_full"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                 if avg["check_full"] > 0 else None},
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(line), flush=True)
+    shard.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -88,6 +88,9 @@ int sbam_open(int device, const uint8_t *data, int64_t len, int64_t base_offset,
               sbam_ctx **out);
 void sbam_close(sbam_ctx *ctx);
 const sbam_error *sbam_last_error(const sbam_ctx *ctx);
+/* Drop every derived stage (block table, stream, bitmap) but keep the compressed bytes and the device
+ * allocations, so the pipeline can be re-run from the resident input without allocating (bench). */
+int sbam_reset(sbam_ctx *ctx);
 const char *sbam_version(void);
 
 /* ---- BGZF layer -------------------------------------------------------------------------------- */

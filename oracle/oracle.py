@@ -87,7 +87,7 @@ class Pos:
 class BamFile:
     """A BGZF/BAM file opened on the CPU oracle: block table, inflated stream, header."""
 
-    def __init__(self, data: bytes | np.ndarray):
+    def __init__(self, data: bytes | np.ndarray, threads: int = 1):
         self.d = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
         self.D = int(self.d.size)
         cap = self.D // 26 + 2
@@ -106,18 +106,44 @@ class BamFile:
         self.uoff[1:] = np.cumsum(self.usize.astype(np.int64))
         self.L = int(self.uoff[-1])
         self.u = np.zeros(max(self.L, 1), np.uint8)
-        eb, ef = np.zeros(1, np.int64), np.zeros(1, np.int64)
-        uo = np.zeros(max(n, 1), np.int64)
-        tot = lib().or_inflate_blocks(_p(self.d), n, _p(self.start), _p(self.csize), _p(self.usize), _p(self.hsize),
-                                      _p(self.u), self.u.size, _p(uo), _p(eb), _p(ef))
-        if tot < 0:
-            b = int(eb[0])
-            raise IOError(f"Expected {int(self.usize[b])} decompressed bytes, found {int(ef[0])}")
+        self._inflate(threads)
         self.lens = np.zeros(1 << 16, np.int64)
         end = np.zeros(1, np.int64)
         nref = lib().or_bam_header(_p(self.u), self.L, _p(self.lens), self.lens.size, _p(end))
         self.nref = int(nref) if nref >= 0 else 0
         self.header_end = int(end[0]) if nref >= 0 else 0
+
+    def _inflate(self, threads: int):
+        """zlib inflate of every block; `threads` > 1 splits the block list across threads (ctypes drops the GIL)."""
+        n = self.nblocks
+        chunks = np.linspace(0, n, max(1, min(threads, n)) + 1).astype(np.int64)
+
+        def run(b0, b1):
+            eb, ef = np.zeros(1, np.int64), np.zeros(1, np.int64)
+            uo = np.zeros(max(b1 - b0, 1), np.int64)
+            out = self.u[int(self.uoff[b0]):]
+            tot = lib().or_inflate_blocks(_p(self.d), b1 - b0, _p(self.start[b0:b1]), _p(self.csize[b0:b1]),
+                                          _p(self.usize[b0:b1]), _p(self.hsize[b0:b1]), out.ctypes.data,
+                                          int(self.uoff[b1] - self.uoff[b0]), _p(uo), _p(eb), _p(ef))
+            if tot < 0:
+                b = b0 + int(eb[0])
+                raise IOError(f"Expected {int(self.usize[b])} decompressed bytes, found {int(ef[0])}")
+        if len(chunks) <= 2:
+            run(0, n)
+        else:
+            from concurrent.futures import ThreadPoolExecutor
+            with ThreadPoolExecutor(len(chunks) - 1) as ex:
+                list(ex.map(lambda i: run(int(chunks[i]), int(chunks[i + 1])), range(len(chunks) - 1)))
+
+    def counts_parallel(self, x0: int, x1: int, reads_to_check: int = 10, threads: int = 1):
+        """counts_range split over `threads` threads (summed)."""
+        from concurrent.futures import ThreadPoolExecutor
+        cuts = np.linspace(x0, x1, max(1, threads) + 1).astype(np.int64)
+        with ThreadPoolExecutor(max(1, threads)) as ex:
+            parts = list(ex.map(lambda i: self.counts_range(int(cuts[i]), int(cuts[i + 1]), reads_to_check),
+                                range(len(cuts) - 1)))
+        c = sum(p[0] for p in parts)
+        return c, sum(p[1] for p in parts), sum(p[2] for p in parts), sum(p[3] for p in parts)
 
     # ---- Pos <-> flat uncompressed offset (UncompressedBytes.scala:17-19; ByteStreamTest.scala:45-53)
     def pos_of(self, x: int) -> Pos:

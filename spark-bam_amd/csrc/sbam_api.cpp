@@ -24,16 +24,24 @@ struct sbam_ctx {
   uint8_t *d_comp = nullptr;
   // candidates from the header scan
   Candidate *d_cand = nullptr;
-  int64_t ncand = 0;
+  int64_t ncand = -1;
+  size_t cand_cap = 0;
+  int32_t *d_cc = nullptr;
+  int64_t *d_coff = nullptr;
+  size_t cc_cap = 0, coff_cap = 0;
   // block table (relative offsets), device + host
   int64_t nblocks = -1;
   int64_t *d_bstart = nullptr, *d_buoff = nullptr;
   int32_t *d_bh = nullptr, *d_bc = nullptr, *d_bu = nullptr;
+  size_t bcap[5] = {0, 0, 0, 0, 0};
   std::vector<int64_t> h_bstart, h_buoff;
   std::vector<int32_t> h_bc, h_bu;
   // uncompressed stream
   uint8_t *d_u = nullptr;
+  size_t u_cap = 0;
   int64_t L = -1;
+  int32_t *d_status = nullptr, *d_found = nullptr;
+  size_t status_cap = 0, found_cap = 0;
   // contig lengths
   int32_t nref = -1;
   int64_t *d_lens = nullptr;
@@ -83,6 +91,16 @@ template <class T>
 void dfree(T *&p) {
   if (p) (void)hipFree(p);
   p = nullptr;
+}
+// grow-only device buffer: reused across sbam_reset() so a re-run allocates nothing
+template <class T>
+hipError_t ensure(T **p, size_t *cap, size_t n) {
+  if (*p && *cap >= n) return hipSuccess;
+  dfree(*p);
+  *cap = 0;
+  hipError_t e = dalloc(p, n);
+  if (e == hipSuccess) *cap = std::max<size_t>(n, 1);
+  return e;
 }
 
 struct Timer {  // HIP events around a launch family on the ctx stream
@@ -200,6 +218,10 @@ void sbam_close(sbam_ctx *c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   dfree(c->d_comp);
   dfree(c->d_cand);
+  dfree(c->d_cc);
+  dfree(c->d_coff);
+  dfree(c->d_status);
+  dfree(c->d_found);
   dfree(c->d_bstart);
   dfree(c->d_buoff);
   dfree(c->d_bh);
@@ -221,6 +243,16 @@ void sbam_close(sbam_ctx *c) {
 
 const sbam_error *sbam_last_error(const sbam_ctx *c) { return c ? &c->err : nullptr; }
 
+int sbam_reset(sbam_ctx *c) {
+  if (!c) return SBAM_ERR_ARG;
+  c->ncand = -1;
+  c->nblocks = -1;
+  c->L = -1;
+  c->bm_valid = false;
+  c->err = sbam_error{};
+  return SBAM_OK;
+}
+
 double sbam_last_kernel_ms(sbam_ctx *c, const char *kernel) {
   auto it = c->ev.find(kernel);
   if (it == c->ev.end()) return -1.0;
@@ -232,24 +264,20 @@ double sbam_last_kernel_ms(sbam_ctx *c, const char *kernel) {
 
 // ---- candidates (scan) ---------------------------------------------------------------------------
 static int scan_candidates(sbam_ctx *c) {
-  if (c->d_cand) return SBAM_OK;
+  if (c->ncand >= 0) return SBAM_OK;
   Timer t(c, "scan");
   const int64_t nchunks = (c->D + kScanChunk - 1) / kScanChunk;
-  int32_t *d_cc = nullptr;
-  int64_t *d_off = nullptr;
-  HIPCHK(c, dalloc(&d_cc, nchunks));
-  HIPCHK(c, dalloc(&d_off, nchunks));
-  HIPCHK(c, launch_scan_count(c->d_comp, c->D, d_cc, nchunks, c->stream));
-  HIPCHK(c, launch_scan_prefix(d_cc, nchunks, d_off, c->d_small, c->stream));
+  HIPCHK(c, ensure(&c->d_cc, &c->cc_cap, nchunks));
+  HIPCHK(c, ensure(&c->d_coff, &c->coff_cap, nchunks));
+  HIPCHK(c, launch_scan_count(c->d_comp, c->D, c->d_cc, nchunks, c->stream));
+  HIPCHK(c, launch_scan_prefix(c->d_cc, nchunks, c->d_coff, c->d_small, c->stream));
   int64_t total = 0;
   HIPCHK(c, hipMemcpyAsync(&total, c->d_small, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  HIPCHK(c, dalloc(&c->d_cand, total));
-  c->ncand = total;
-  HIPCHK(c, launch_scan_write(c->d_comp, c->D, d_off, nchunks, c->d_cand, c->stream));
+  HIPCHK(c, ensure(&c->d_cand, &c->cand_cap, total));
+  HIPCHK(c, launch_scan_write(c->d_comp, c->D, c->d_coff, nchunks, c->d_cand, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  dfree(d_cc);
-  dfree(d_off);
+  c->ncand = total;
   return SBAM_OK;
 }
 
@@ -322,11 +350,14 @@ int sbam_scan_blocks(sbam_ctx *c, int64_t *n_blocks) {
     else if (code == 2) nb = si - first + 1;
     else fast = false;  // a candidate that is not the next header: walk exactly on the host
   }
+  c->h_bstart.clear();
+  c->h_bc.clear();
+  c->h_bu.clear();
+  HIPCHK(c, ensure(&c->d_bstart, &c->bcap[0], nb + 1));
+  HIPCHK(c, ensure(&c->d_bh, &c->bcap[1], nb + 1));
+  HIPCHK(c, ensure(&c->d_bc, &c->bcap[2], nb + 1));
+  HIPCHK(c, ensure(&c->d_bu, &c->bcap[3], nb + 1));
   if (fast) {
-    HIPCHK(c, dalloc(&c->d_bstart, nb));
-    HIPCHK(c, dalloc(&c->d_bh, nb));
-    HIPCHK(c, dalloc(&c->d_bc, nb));
-    HIPCHK(c, dalloc(&c->d_bu, nb));
     HIPCHK(c, launch_gather_blocks(c->d_cand, first, nb, c->d_bstart, c->d_bh, c->d_bc, c->d_bu, c->stream));
     c->h_bstart.resize(nb);
     c->h_bc.resize(nb);
@@ -353,10 +384,10 @@ int sbam_scan_blocks(sbam_ctx *c, int64_t *n_blocks) {
       q += k.csize;
     }
     nb = (int64_t)c->h_bstart.size();
-    HIPCHK(c, dalloc(&c->d_bstart, nb));
-    HIPCHK(c, dalloc(&c->d_bh, nb));
-    HIPCHK(c, dalloc(&c->d_bc, nb));
-    HIPCHK(c, dalloc(&c->d_bu, nb));
+    HIPCHK(c, ensure(&c->d_bstart, &c->bcap[0], nb + 1));
+    HIPCHK(c, ensure(&c->d_bh, &c->bcap[1], nb + 1));
+    HIPCHK(c, ensure(&c->d_bc, &c->bcap[2], nb + 1));
+    HIPCHK(c, ensure(&c->d_bu, &c->bcap[3], nb + 1));
     HIPCHK(c, hipMemcpy(c->d_bstart, c->h_bstart.data(), nb * 8, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_bh, h_h.data(), nb * 4, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_bc, c->h_bc.data(), nb * 4, hipMemcpyHostToDevice));
@@ -369,7 +400,7 @@ int sbam_scan_blocks(sbam_ctx *c, int64_t *n_blocks) {
     acc += (c->h_bu[b] < 0) ? 0 : c->h_bu[b];
   }
   c->h_buoff[nb] = acc;
-  HIPCHK(c, dalloc(&c->d_buoff, nb + 1));
+  HIPCHK(c, ensure(&c->d_buoff, &c->bcap[4], nb + 1));
   HIPCHK(c, hipMemcpyAsync(c->d_buoff, c->h_buoff.data(), (nb + 1) * 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->nblocks = nb;
@@ -397,10 +428,8 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
   if (rc) return rc;
   HIPCHK(c, hipSetDevice(c->device));
   const int64_t L = c->h_buoff[c->nblocks];
-  if (!c->d_u) {
-    HIPCHK(c, dalloc(&c->d_u, (size_t)L + kStreamPad));
-    HIPCHK(c, hipMemsetAsync(c->d_u + L, 0, kStreamPad, c->stream));
-  }
+  HIPCHK(c, ensure(&c->d_u, &c->u_cap, (size_t)L + kStreamPad));
+  HIPCHK(c, hipMemsetAsync(c->d_u + L, 0, kStreamPad, c->stream));
   const int64_t nb = c->nblocks;
   int lanes = (int)std::min<int64_t>(((nb + 255) / 256) * 256, 256LL * 256 * 2);  // ≤ 512 lanes per CU
   if (lanes < 256) lanes = 256;
@@ -409,9 +438,9 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
     HIPCHK(c, dalloc(&c->d_scratch, (size_t)lanes * kInflateScratchU16));
     c->nlanes = lanes;
   }
-  int32_t *d_status = nullptr, *d_found = nullptr;
-  HIPCHK(c, dalloc(&d_status, nb));
-  HIPCHK(c, dalloc(&d_found, nb));
+  HIPCHK(c, ensure(&c->d_status, &c->status_cap, nb));
+  HIPCHK(c, ensure(&c->d_found, &c->found_cap, nb));
+  int32_t *d_status = c->d_status, *d_found = c->d_found;
   const unsigned long long none = ~0ull;
   HIPCHK(c, hipMemcpyAsync(c->d_small + 2, &none, 8, hipMemcpyHostToDevice, c->stream));
   BlockTable bt{c->d_bstart, c->d_bh, c->d_bc, c->d_bu, c->d_buoff, nb};
@@ -430,12 +459,8 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
     c->err.position = c->base + c->h_bstart[ferr];
     c->err.expected = c->h_bu[ferr];
     c->err.actual = found;
-    dfree(d_status);
-    dfree(d_found);
     return set_err(c, SBAM_ERR_INFLATE, "Expected %d decompressed bytes, found %d", c->h_bu[ferr], found);
   }
-  dfree(d_status);
-  dfree(d_found);
   c->L = L;
   c->bm_valid = false;
   if (usz) *usz = L;

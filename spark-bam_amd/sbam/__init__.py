@@ -100,7 +100,7 @@ class _SplitArgs(ctypes.Structure):
 
 
 EXPORTS = [  # every symbol include/sbam.h declares
-    "sbam_open", "sbam_close", "sbam_last_error", "sbam_version", "sbam_find_block_starts", "sbam_scan_blocks",
+    "sbam_open", "sbam_close", "sbam_last_error", "sbam_reset", "sbam_version", "sbam_find_block_starts", "sbam_scan_blocks",
     "sbam_get_blocks", "sbam_inflate", "sbam_read_uncompressed", "sbam_pos_to_offset", "sbam_offset_to_pos",
     "sbam_header", "sbam_set_contig_lengths", "sbam_check_eager", "sbam_check_full_words", "sbam_check_full_counts",
     "sbam_find_record_start", "sbam_file_splits", "sbam_split_records", "sbam_compute_splits",
@@ -123,6 +123,7 @@ def load_library(path: str = LIB_PATH):
         "sbam_open": (ctypes.c_int, [ctypes.c_int, vp, i64, i64, i64, P(vp)]),
         "sbam_close": (None, [vp]),
         "sbam_last_error": (P(_Error), [vp]),
+        "sbam_reset": (ctypes.c_int, [vp]),
         "sbam_version": (ctypes.c_char_p, []),
         "sbam_find_block_starts": (ctypes.c_int, [vp, vp, i64, i32, vp]),
         "sbam_scan_blocks": (ctypes.c_int, [vp, P(i64)]),
@@ -276,6 +277,21 @@ class BamFile:
             self.close()
         except Exception:
             pass
+
+    def reset(self):
+        """Drop derived stages (keeps the resident compressed bytes and allocations)."""
+        self._check(self.L.sbam_reset(self.ctx))
+        self.n_blocks = None
+        self.uncompressed_size = None
+
+    def run(self, contig_lengths: Optional[Sequence[int]] = None):
+        """Scan → inflate → header/contig lengths from the resident compressed bytes."""
+        self.n_blocks = self._scan()
+        self.inflate()
+        if contig_lengths is not None:
+            self.set_contig_lengths(contig_lengths)
+        elif self.base_offset == 0:
+            self.header()
 
     def kernel_ms(self, name: str) -> float:
         return float(self.L.sbam_last_kernel_ms(self.ctx, name.encode()))

@@ -1,0 +1,186 @@
+"""Multi-GPU driver: one process per GPU, byte-range shards of one BAM, tiny collectives.
+
+Shard planning follows the reference's partitioning (one task per Hadoop FileSplit,
+load/.../spark/load/SplitRDD.scala:33-52): rank r owns a contiguous run of Hadoop splits; it loads the
+compressed bytes of those splits plus a halo (records and 10-record checker chains straddle shard edges),
+starts its BGZF stream at FindBlockStart(first split start) and stops checking at the block where rank
+r+1 starts.  The only cross-GPU traffic is what Spark's driver does with tiny data:
+
+* ``all_gather`` of each split's first-record Pos / non-empty flag / record count
+  (``mapPartitions(first).collect``, CanLoadBam.scala:262-271);
+* ``all_reduce(sum)`` of the full-check Counts table (``reduceByKey(_ |+| _)``, FullCheck.scala:160-168).
+
+A chain that leaves the loaded bytes reports HALO; the shard doubles its halo and re-runs (adaptive halo
+for long reads).  ``compute`` is pluggable so the distributed logic is testable on CPU (gloo) with a
+CPU-side per-shard function; production uses ``GpuShard``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+
+N_COUNT_WORDS = 21 * 19 + 21 + 21 * 128 + 19 * 19 + 3
+
+
+def hadoop_splits(file_size: int, split_size: int):
+    """FileInputFormat rule (SPLIT_SLOP 1.1), same arithmetic as sbam_file_splits."""
+    out, off, rem = [], 0, file_size
+    while rem / split_size > 1.1:
+        out.append((off, off + split_size))
+        off += split_size
+        rem -= split_size
+    if rem > 0:
+        out.append((off, file_size))
+    return out
+
+
+@dataclass
+class ShardPlan:
+    rank: int
+    world: int
+    split_first: int  # first Hadoop split index owned
+    split_count: int
+    lo: int  # first compressed byte owned (start of the first owned split)
+    owned_hi: int  # start of the next rank's first split (or file size)
+    file_size: int
+
+    def load_range(self, halo: int):
+        return self.lo, min(self.file_size, self.owned_hi + halo)
+
+
+def plan_shards(file_size: int, split_size: int, world: int) -> List[ShardPlan]:
+    sp = hadoop_splits(file_size, split_size)
+    ns = len(sp)
+    plans = []
+    for r in range(world):
+        i0, i1 = r * ns // world, (r + 1) * ns // world
+        lo = sp[i0][0] if i0 < ns else file_size
+        hi = sp[i1][0] if i1 < ns else file_size
+        plans.append(ShardPlan(r, world, i0, i1 - i0, lo, hi, file_size))
+    return plans
+
+
+@dataclass
+class ShardResult:
+    counts: np.ndarray  # int64[N_COUNT_WORDS] (by_key, positions, rbe, pair, n_success, n_tff, n_positions)
+    first_block_pos: np.ndarray  # int64[split_count]
+    first_offset: np.ndarray  # int64[split_count]
+    nonempty: np.ndarray  # int64[split_count]
+    n_records: np.ndarray  # int64[split_count]
+
+
+def pack_counts(c) -> np.ndarray:
+    return np.concatenate([c.by_key.ravel(), c.positions, c.reads_before_error.ravel(), c.pair_hist.ravel(),
+                           np.array([c.n_success, c.n_too_few_fixed, c.n_positions], np.int64)]).astype(np.int64)
+
+
+def unpack_counts(v: np.ndarray) -> dict:
+    o = 0
+    out = {}
+    for name, n, shape in (("by_key", 21 * 19, (21, 19)), ("positions", 21, (21,)),
+                           ("reads_before_error", 21 * 128, (21, 128)), ("pair_hist", 19 * 19, (19, 19))):
+        out[name] = v[o:o + n].reshape(shape)
+        o += n
+    out["n_success"], out["n_too_few_fixed"], out["n_positions"] = (int(x) for x in v[o:o + 3])
+    return out
+
+
+class GpuShard:
+    """Per-rank GPU work for one shard: scan → inflate → full check (owned positions) → split records."""
+
+    def __init__(self, plan: ShardPlan, source: Callable[[int, int], np.ndarray], split_size: int,
+                 contig_lengths: Sequence[int], device: int = 0, halo: int = 2 << 20, reads_to_check: int = 10):
+        import sbam
+        self.sbam = sbam
+        self.plan, self.source, self.split_size = plan, source, split_size
+        self.contig_lengths = np.asarray(contig_lengths, np.int64)
+        self.device, self.halo, self.R = device, halo, reads_to_check
+        self.f = None
+        self._open()
+
+    def _open(self):
+        lo, hi = self.plan.load_range(self.halo)
+        if self.f is not None:
+            self.f.close()
+        self.f = self.sbam.BamFile(self.source(lo, hi), device=self.device, base_offset=lo,
+                                   file_size=self.plan.file_size, inflate=False)
+
+    def _once(self) -> ShardResult:
+        p, f = self.plan, self.f
+        f.reset()
+        f.run(contig_lengths=self.contig_lengths)
+        st, _, _, uo = f.blocks()
+        if p.owned_hi >= p.file_size:
+            x1 = f.uncompressed_size
+        else:
+            nb = f.find_block_start(p.owned_hi)
+            b = int(np.searchsorted(st, nb))
+            x1 = int(uo[b]) if b < st.size else f.uncompressed_size
+        counts = f.check_full_counts(0, x1, self.R)
+        recs = f.split_records(self.split_size, first=p.split_first, count=p.split_count,
+                               reads_to_check=self.R, use_success_bitmap=True) if p.split_count else []
+        return ShardResult(pack_counts(counts),
+                           np.array([r[0].block_pos for r in recs], np.int64),
+                           np.array([r[0].offset for r in recs], np.int64),
+                           np.array([int(r[1]) for r in recs], np.int64),
+                           np.array([r[2] for r in recs], np.int64))
+
+    def step(self) -> ShardResult:
+        while True:
+            try:
+                return self._once()
+            except self.sbam.HaloException:
+                if self.plan.load_range(self.halo)[1] >= self.plan.file_size:
+                    raise
+                self.halo *= 4
+                self._open()
+
+    def close(self):
+        if self.f is not None:
+            self.f.close()
+            self.f = None
+
+
+def combine(results: Sequence[ShardResult], file_size: int):
+    """Rank-0 assembly of gathered shard results → (Split list, partition sizes, merged counts)."""
+    from sbam import Pos, Split
+    firsts, sizes = [], []
+    counts = np.zeros(N_COUNT_WORDS, np.int64)
+    for r in results:
+        counts += r.counts
+        for b, o, ne, n in zip(r.first_block_pos, r.first_offset, r.nonempty, r.n_records):
+            sizes.append(int(n))
+            if ne:
+                firsts.append(Pos(int(b), int(o)))
+    ends = firsts[1:] + [Pos(file_size, 0)]
+    return [Split(a, b) for a, b in zip(firsts, ends)], sizes, counts
+
+
+def gather_results(res: ShardResult, plans: Sequence[ShardPlan], device=None) -> Optional[List[ShardResult]]:
+    """all_gather of per-shard results (fixed-size int64 rows) + all_reduce of counts via torch.distributed.
+    Returns the per-rank list on every rank (counts of each entry are the merged totals on rank 0's row)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    maxs = max(p.split_count for p in plans)
+    row = np.zeros(4 * maxs, np.int64)
+    k = len(res.n_records)
+    for j, a in enumerate((res.first_block_pos, res.first_offset, res.nonempty, res.n_records)):
+        row[j * maxs: j * maxs + k] = a
+    t = torch.from_numpy(row)
+    c = torch.from_numpy(res.counts.copy())
+    if device is not None:
+        t, c = t.to(device), c.to(device)
+    out = torch.empty(world * row.size, dtype=torch.int64, device=t.device)
+    dist.all_gather_into_tensor(out, t)
+    dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    out = out.cpu().numpy().reshape(world, 4, maxs)
+    merged = c.cpu().numpy()
+    results = []
+    for r, p in enumerate(plans):
+        n = p.split_count
+        results.append(ShardResult(merged if r == 0 else np.zeros_like(merged), out[r, 0, :n], out[r, 1, :n],
+                                   out[r, 2, :n], out[r, 3, :n]))
+    return results

@@ -4,7 +4,7 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for p in (os.path.join(ROOT, "oracle"), os.path.join(ROOT, "spark-bam_amd"), ROOT):
+for p in (os.path.join(ROOT, "oracle"), os.path.join(ROOT, "spark-bam_amd"), os.path.join(ROOT, "tools"), ROOT):
     if p not in sys.path:
         sys.path.insert(0, p)
 

@@ -1,0 +1,97 @@
+"""Synthetic BAM workloads for bench.py and the large-size tests (SURVEY §8(d) config specs).
+
+A synthetic file is   header blocks | tile × k | EOF marker   where a tile is a run of records cut into
+65498-byte payloads compressed at zlib level 6 (tools/synth_bam.c).  The tile ends on a record boundary, so
+the record chain runs through every seam; any byte range of the file can be produced without
+materialising the whole file (``SynthBam.slice``), which is how each rank builds its shard + halo."""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "libsynth.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            subprocess.run(["make", "-s", "-C", HERE], check=True)
+        L = ctypes.CDLL(LIB)
+        vp, i64 = ctypes.c_void_p, ctypes.c_int64
+        L.synth_header.restype = i64
+        L.synth_header.argtypes = [ctypes.POINTER(vp)]
+        L.synth_tile.restype = i64
+        L.synth_tile.argtypes = [ctypes.c_uint64, i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp),
+                                 ctypes.POINTER(i64), ctypes.POINTER(i64)]
+        L.synth_contigs.argtypes = [ctypes.POINTER(ctypes.c_int32), vp]
+        L.synth_free.argtypes = [vp]
+        L.synth_eof.restype = vp
+        _lib = L
+    return _lib
+
+
+def _take(p, n) -> np.ndarray:
+    a = np.frombuffer(ctypes.string_at(p, n), np.uint8).copy()
+    lib().synth_free(p)
+    return a
+
+
+class SynthBam:
+    def __init__(self, tile_mb: float = 64.0, copies: int = 1, read_len: int = 150, seed: int = 0x5EEDBA11,
+                 level: int = 6, threads: int = 16):
+        L = lib()
+        p = ctypes.c_void_p()
+        n = L.synth_header(ctypes.byref(p))
+        self.header = _take(p, n)
+        nrec, ulen = ctypes.c_int64(0), ctypes.c_int64(0)
+        n = L.synth_tile(seed, int(tile_mb * 3 * 2 ** 20), read_len, level, threads, ctypes.byref(p),
+                         ctypes.byref(nrec), ctypes.byref(ulen))
+        self.tile = _take(p, n)
+        self.eof = np.frombuffer(ctypes.string_at(L.synth_eof(), 28), np.uint8).copy()
+        self.tile_records = nrec.value
+        self.tile_u = ulen.value
+        self.copies = copies
+        self.size = self.header.size + copies * self.tile.size + 28
+        self.n_records = copies * self.tile_records
+        nr = ctypes.c_int32(0)
+        lens = np.zeros(128, np.int64)
+        L.synth_contigs(ctypes.byref(nr), lens.ctypes.data)
+        self.contig_lengths = lens[: nr.value]
+
+    @staticmethod
+    def for_size(target_bytes: int, tile_mb: float = 64.0, **kw) -> "SynthBam":
+        s = SynthBam(tile_mb=tile_mb, copies=1, **kw)
+        s.copies = max(1, round((target_bytes - s.header.size - 28) / s.tile.size))
+        s.size = s.header.size + s.copies * s.tile.size + 28
+        s.n_records = s.copies * s.tile_records
+        return s
+
+    def slice(self, lo: int, hi: int, out: np.ndarray | None = None) -> np.ndarray:
+        """File bytes [lo, hi) (hi clamped to the file size)."""
+        hi = min(hi, self.size)
+        out = np.empty(hi - lo, np.uint8) if out is None else out
+        H, T = self.header.size, self.tile.size
+        pos = lo
+        while pos < hi:
+            if pos < H:
+                n = min(hi, H) - pos
+                out[pos - lo: pos - lo + n] = self.header[pos: pos + n]
+            elif pos < H + self.copies * T:
+                k, o = divmod(pos - H, T)
+                n = min(hi - pos, T - o)
+                out[pos - lo: pos - lo + n] = self.tile[o: o + n]
+            else:
+                o = pos - H - self.copies * T
+                n = hi - pos
+                out[pos - lo: pos - lo + n] = self.eof[o: o + n]
+            pos += n
+        return out
+
+    def bytes(self) -> np.ndarray:
+        return self.slice(0, self.size)
