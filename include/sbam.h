@@ -64,7 +64,8 @@ typedef struct {
 #define SBAM_NUM_KEYS 21
 #define SBAM_MAX_READS_TO_CHECK 127
 typedef struct {
-  int64_t counts[SBAM_NUM_KEYS][SBAM_NUM_FLAGS];            /* per key, per flag */
+  int64_t totals[SBAM_NUM_FLAGS];                           /* per flag, all keys ("Total error counts") */
+  int64_t counts[SBAM_NUM_KEYS][SBAM_NUM_FLAGS];            /* per key, per flag: keys 1-2 always, all with by_key */
   int64_t positions[SBAM_NUM_KEYS];                         /* positions per key */
   int64_t reads_before_error[SBAM_NUM_KEYS][SBAM_MAX_READS_TO_CHECK + 1];
   int64_t pair_hist[SBAM_NUM_FLAGS][SBAM_NUM_FLAGS];        /* key-2 positions by (flag i < flag j) */
@@ -136,9 +137,11 @@ int sbam_check_eager(sbam_ctx *ctx, int64_t x0, int64_t x1, int32_t reads_to_che
 int sbam_check_full_words(sbam_ctx *ctx, int64_t x0, int64_t x1, int32_t reads_to_check, uint32_t *words);
 
 /* full.Checker over [x0, x1) reduced to full-check Counts + success bitmap (device-resident; copied
- * to success_bitmap when non-NULL).  Replaces the per-position RDD + reduceByKey of FullCheck.scala:117-191. */
-int sbam_check_full_counts(sbam_ctx *ctx, int64_t x0, int64_t x1, int32_t reads_to_check, sbam_counts *counts,
-                           uint64_t *success_bitmap);
+ * to success_bitmap when non-NULL).  Replaces the per-position RDD + reduceByKey of FullCheck.scala:117-191.
+ * by_key = 0 fills what the full-check report prints (totals, keys 1-2 per flag, positions per key, close-call
+ * pairs, readsBeforeError); by_key = 1 also fills counts[k][f] for every key (negativesByNumNonzeroFields). */
+int sbam_check_full_counts(sbam_ctx *ctx, int64_t x0, int64_t x1, int32_t reads_to_check, int32_t by_key,
+                           sbam_counts *counts, uint64_t *success_bitmap);
 
 /* FindRecordStart.withDelta (check/.../bam/spark/FindRecordStart.scala:30-63) from Pos(block_start, 0):
  * *found = 0 means None. */

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -66,7 +67,7 @@ struct sbam_ctx {
 
 namespace {
 
-constexpr size_t kCountsWords = 21 * 19 + 21 + 21 * 128 + 19 * 19 + 4;
+constexpr size_t kCountsWords = 21 * 19 + 21 + 21 * 128 + 19 * 19 + 4 + 19;
 
 int set_err(sbam_ctx *c, int code, const char *fmt, ...) {
   c->err.code = code;
@@ -178,7 +179,7 @@ sbam_pos pos_of(const sbam_ctx *c, int64_t x) {
 }
 
 int ensure_bitmap(sbam_ctx *c, int64_t x0, int64_t x1) {
-  const size_t words = (size_t)((x1 - x0 + 63) / 64) + 1;
+  const size_t words = (size_t)((x1 - (x0 & ~(int64_t)63) + 63) / 64) + 1;
   if (words > c->bitmap_cap) {
     dfree(c->d_bitmap);
     HIPCHK(c, dalloc(&c->d_bitmap, words));
@@ -431,7 +432,9 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
   HIPCHK(c, ensure(&c->d_u, &c->u_cap, (size_t)L + kStreamPad));
   HIPCHK(c, hipMemsetAsync(c->d_u + L, 0, kStreamPad, c->stream));
   const int64_t nb = c->nblocks;
-  int lanes = (int)std::min<int64_t>(((nb + 255) / 256) * 256, 256LL * 256 * 2);  // ≤ 512 lanes per CU
+  int64_t cap_lanes = 256LL * 512;  // ≤ 512 lanes (8 waves) per CU
+  if (const char *e = getenv("SBAM_INFLATE_LANES")) cap_lanes = std::max<int64_t>(256, atoll(e));
+  int lanes = (int)std::min<int64_t>(((nb + 255) / 256) * 256, (cap_lanes / 256) * 256);
   if (lanes < 256) lanes = 256;
   if (lanes > c->nlanes) {
     dfree(c->d_scratch);
@@ -542,6 +545,25 @@ int sbam_header(sbam_ctx *c, int32_t *n_ref, int64_t *lengths, int32_t cap, sbam
   return SBAM_OK;
 }
 
+// Copy a device bitmap covering [x0 & ~63, x1) out as bits relative to x0.
+static int copy_bitmap_out(sbam_ctx *c, int64_t x0, int64_t x1, uint64_t *out) {
+  const int64_t x0a = x0 & ~(int64_t)63, sh = x0 - x0a;
+  const size_t nwa = (size_t)((x1 - x0a + 63) / 64), nw = (size_t)((x1 - x0 + 63) / 64);
+  if (!nw) return SBAM_OK;
+  if (!sh) {
+    HIPCHK(c, hipMemcpyAsync(out, c->d_bitmap, nw * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return SBAM_OK;
+  }
+  std::vector<uint64_t> t(nwa + 1, 0);
+  HIPCHK(c, hipMemcpyAsync(t.data(), c->d_bitmap, nwa * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (size_t i = 0; i < nw; i++) out[i] = (t[i] >> sh) | (t[i + 1] << (64 - sh));
+  const int64_t tail = (x1 - x0) & 63;
+  if (tail) out[nw - 1] &= (1ull << tail) - 1;
+  return SBAM_OK;
+}
+
 // ---- checkers ------------------------------------------------------------------------------------
 static int check_range_args(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R) {
   int rc = ensure_stream(c);
@@ -562,10 +584,12 @@ int sbam_check_eager(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, uint64_t *b
     Timer t(c, "check_eager");
     HIPCHK(c, launch_check_eager(view(c), x0, x1, R, c->d_bitmap, c->stream));
   }
-  const size_t words = (size_t)((x1 - x0 + 63) / 64);
-  if (bitmap && words) HIPCHK(c, hipMemcpyAsync(bitmap, c->d_bitmap, words * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  c->bm_x0 = x0;
+  if (bitmap) {
+    int rc2 = copy_bitmap_out(c, x0, x1, bitmap);
+    if (rc2) return rc2;
+  }
+  c->bm_x0 = x0 & ~(int64_t)63;
   c->bm_x1 = x1;
   c->bm_R = R;
   c->bm_valid = true;
@@ -579,17 +603,24 @@ int sbam_check_full_words(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, uint32
   HIPCHK(c, hipSetDevice(c->device));
   uint32_t *d_w = nullptr;
   HIPCHK(c, dalloc(&d_w, x1 - x0));
+  rc = ensure_bitmap(c, x0, x1);
+  if (rc) return rc;
   {
     Timer t(c, "check_words");
-    HIPCHK(c, launch_check_words(view(c), x0, x1, R, d_w, c->stream));
+    HIPCHK(c, launch_check_words(view(c), x0, x1, R, d_w, c->d_bitmap, c->stream));
   }
+  c->bm_x0 = x0 & ~(int64_t)63;
+  c->bm_x1 = x1;
+  c->bm_R = R;
+  c->bm_valid = true;
   if (x1 > x0) HIPCHK(c, hipMemcpyAsync(words, d_w, (x1 - x0) * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   dfree(d_w);
   return SBAM_OK;
 }
 
-int sbam_check_full_counts(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, sbam_counts *out, uint64_t *bitmap) {
+int sbam_check_full_counts(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, int32_t by_key, sbam_counts *out,
+                           uint64_t *bitmap) {
   if (!c || !out) return SBAM_ERR_ARG;
   int rc = check_range_args(c, x0, x1, R);
   if (rc) return rc;
@@ -603,15 +634,18 @@ int sbam_check_full_counts(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, sbam_
   cd.rbe = cd.positions + 21;
   cd.pair = cd.rbe + 21 * 128;
   cd.scalars = cd.pair + 19 * 19;
+  cd.totals = cd.scalars + 4;
   {
     Timer t(c, "check_full");
-    HIPCHK(c, launch_check_full_counts(view(c), x0, x1, R, cd, c->d_bitmap, c->stream));
+    HIPCHK(c, launch_check_full_counts(view(c), x0, x1, R, by_key, cd, c->d_bitmap, c->stream));
   }
   std::vector<unsigned long long> h(kCountsWords);
   HIPCHK(c, hipMemcpyAsync(h.data(), c->d_counts, kCountsWords * 8, hipMemcpyDeviceToHost, c->stream));
-  const size_t words = (size_t)((x1 - x0 + 63) / 64);
-  if (bitmap && words) HIPCHK(c, hipMemcpyAsync(bitmap, c->d_bitmap, words * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (bitmap) {
+    int rc2 = copy_bitmap_out(c, x0, x1, bitmap);
+    if (rc2) return rc2;
+  }
   memset(out, 0, sizeof(*out));
   const unsigned long long *p = h.data();
   for (int k = 0; k < 21; k++)
@@ -629,7 +663,9 @@ int sbam_check_full_counts(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, sbam_
   out->n_success = (int64_t)p[1];
   out->n_too_few_fixed = (int64_t)p[2];
   out->n_halo = (int64_t)p[3];
-  c->bm_x0 = x0;
+  p += 4;
+  for (int f = 0; f < 19; f++) out->totals[f] = (int64_t)p[f];
+  c->bm_x0 = x0 & ~(int64_t)63;
   c->bm_x1 = x1;
   c->bm_R = R;
   c->bm_valid = true;

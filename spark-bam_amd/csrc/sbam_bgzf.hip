@@ -1,13 +1,9 @@
-// sbam_kernels.hip — hand-written CDNA4 (gfx950) kernels for the spark-bam hot path.
+// sbam_bgzf.hip — hand-written CDNA4 (gfx950) kernels for the BGZF layer of the spark-bam hot path.
 //
 //  * BGZF block-header scan   (Header.make bgzf/.../block/Header.scala:48-83, MetadataStream.scala:23-54,
 //                              FindBlockStart.scala:8-36)
 //  * batched raw-DEFLATE inflate (Stream.scala:31-71; RFC 1951 semantics of java.util.zip.Inflater)
-//  * exhaustive per-offset record-boundary checker, eager + full
-//                             (check/.../check/eager/Checker.scala:24-126, full/Checker.scala:22-184,
-//                              PosChecker.scala:43-63) with full-check Counts reduction (FullCheck.scala:141-191)
-//  * FindRecordStart scan     (check/.../bam/spark/FindRecordStart.scala:30-63)
-//  * record-chain walk        (check/.../bam/iterator/RecordStream.scala:27-41)
+//  The record-boundary checker and record chain live in sbam_check.hip.
 //
 // All byte/integer work: no MFMA (no dense contraction).  Design notes and rooflines: DESIGN.md.
 #include "sbam_internal.h"
@@ -579,340 +575,8 @@ __global__ __launch_bounds__(256) void k_inflate(const uint8_t *__restrict__ d, 
 }
 
 // ================================================================================================
-// 3. Record-boundary checker
-// ================================================================================================
-constexpr uint32_t W_SUCC = 0x80000000u, W_HALO = 0x00800000u;
-constexpr int kCheckThreads = 256;
-constexpr int kTile = 8192;  // positions per workgroup tile
-constexpr int kHalo = 768;   // staged bytes past the tile: fixed fields + max read name (36 + 255) + cigar ops
-constexpr int kWin = kTile + 16 + kHalo;  // staged window (multiple of 16)
-static_assert(kWin % 16 == 0, "window");
-
-// Bytes of the stream: the staged LDS window when inside it, else global memory.
-struct Win {
-  const uint8_t *lds;
-  int64_t base;  // stream offset of lds[0]
-  int wlen;
-  const uint8_t *g;
-  SB_DEV uint32_t byte(int64_t x) const {
-    const int64_t r = x - base;
-    return (r >= 0 && r < wlen) ? (uint32_t)lds[r] : (uint32_t)g[x];
-  }
-  SB_DEV int32_t i32(int64_t x) const {
-    return (int32_t)(byte(x) | (byte(x + 1) << 8) | (byte(x + 2) << 16) | (byte(x + 3) << 24));
-  }
-};
-
-SB_DEV bool name_char_ok(uint32_t b) { return (b - 33u <= 30u) || (b - 65u <= 61u); }
-
-// PosChecker.getRefPosError as bits {negIdx, bigIdx, negPos, bigPos}; note negPos = rp < -1 in every branch.
-SB_DEV uint32_t ref_err(int32_t ri, int32_t rp, const int64_t *lens, int32_t nref) {
-  uint32_t f = 0;
-  f |= (ri < -1) ? 1u : 0u;
-  f |= (ri >= nref) ? 2u : 0u;
-  f |= (rp < -1) ? 4u : 0u;
-  if (ri >= 0 && ri < nref && rp >= -1) f |= ((int64_t)rp > lens[ri]) ? 8u : 0u;
-  return f;
-}
-
-// full.Checker from position p with the k=0 fixed fields already loaded (f[0..7] = block_size, refID, pos,
-// bin_mq_nl, flag_nc, l_seq, next_refID, next_pos).  EAGER: stop at the first failing group (the boolean
-// is the same; flags returned are partial).  Returns the result word (sbam.h).
-template <bool EAGER>
-SB_DEV uint32_t check_from(const Win &w, const StreamView &sv, int64_t p, int R, const int32_t f0[8]) {
-  int64_t s = p, a = p;
-  int k = 0;
-  int32_t bs = f0[0], ri = f0[1], rp = f0[2], bmn = f0[3], fnc = f0[4], ls = f0[5], nri = f0[6], nrp = f0[7];
-  for (;;) {
-    if (k == R) return W_SUCC | ((uint32_t)k << 24);
-    if (a + 36 > sv.L) {
-      if (!sv.eof_real) return W_HALO;
-      if (k > 0 && s == sv.L) return W_SUCC | ((uint32_t)k << 24);
-      return 1u | ((uint32_t)k << 24);
-    }
-    if (k > 0) {
-      bs = w.i32(a); ri = w.i32(a + 4); rp = w.i32(a + 8); bmn = w.i32(a + 12);
-      fnc = w.i32(a + 16); ls = w.i32(a + 20); nri = w.i32(a + 24); nrp = w.i32(a + 28);
-    }
-    uint32_t F = ref_err(ri, rp, sv.lens, sv.nref) << 1;
-    if (EAGER && F) return (uint32_t)k << 24 | F;
-    const int32_t lrn = bmn & 0xff;
-    const uint32_t flag = ((uint32_t)fnc) >> 16;
-    const int32_t nc = fnc & 0xffff;
-    const int32_t t = (int32_t)((uint32_t)ls + 1u);
-    const int32_t nsq = (int32_t)((uint32_t)(t / 2) + (uint32_t)ls);
-    const int32_t implied = (int32_t)(32u + (uint32_t)lrn + 4u * (uint32_t)nc + (uint32_t)nsq);
-    F |= (bs < implied) ? (1u << 18) : 0u;
-    F |= ref_err(nri, nrp, sv.lens, sv.nref) << 5;
-    if (EAGER) {
-      if (F || lrn < 2 || ((flag & 4u) == 0 && (ls == 0 || nc == 0))) return ((uint32_t)k << 24) | (F ? F : 1u << 12);
-    }
-    int64_t c = a + 36;
-    if (lrn == 0) {
-      F |= 1u << 12;
-    } else if (lrn == 1) {
-      F |= 1u << 13;
-    } else {
-      if (c + lrn > sv.L) {
-        if (!sv.eof_real) return W_HALO;
-        return F | (1u << 9) | ((uint32_t)k << 24);
-      }
-      if (w.byte(c + lrn - 1) != 0) {
-        F |= 1u << 10;
-      } else {
-        for (int32_t i = 0; i < lrn - 1; i++)
-          if (!name_char_ok(w.byte(c + i))) {
-            F |= 1u << 11;
-            break;
-          }
-      }
-      c += lrn;
-      if (EAGER && F) return ((uint32_t)k << 24) | F;
-    }
-    bool cig_err = false;
-    for (int32_t i = 0; i < nc; i++) {
-      if (c + 4 > sv.L) {
-        if (!sv.eof_real) return W_HALO;
-        F |= 1u << 14;
-        cig_err = true;
-        break;
-      }
-      const uint32_t op = w.byte(c);
-      c += 4;
-      if ((op & 0xfu) > 8u) {
-        F |= 1u << 15;
-        cig_err = true;
-        break;
-      }
-    }
-    if (!cig_err && (flag & 4u) == 0 && (ls == 0 || nc == 0)) {
-      F |= (ls == 0) ? (1u << 16) : 0u;  // EmptyMapped(emptySeq, emptyCigar) → (emptyMappedCigar, emptyMappedSeq)
-      F |= (nc == 0) ? (1u << 17) : 0u;
-    }
-    if (F) return F | ((uint32_t)k << 24);
-    const int64_t nxt = s + 4 + (int64_t)bs;
-    if (nxt > c) {
-      if (nxt > sv.L && !sv.eof_real) return W_HALO;
-      a = nxt > sv.L ? sv.L : nxt;
-    } else {
-      a = c;
-    }
-    s = nxt;
-    k++;
-  }
-}
-
-// Stage stream bytes [abase, abase + kWin) into LDS (16 B per lane per step; the stream is zero padded).
-SB_DEV void stage(uint8_t *s_win, const uint8_t *u, int64_t abase) {
-  const uint4 *src = reinterpret_cast<const uint4 *>(u + abase);
-  uint4 *dst = reinterpret_cast<uint4 *>(s_win);
-  for (int i = threadIdx.x; i < kWin / 16; i += kCheckThreads) dst[i] = src[i];
-}
-
-// k=0 fixed fields of position x from the staged window: ten aligned LDS dwords + v_alignbyte.
-SB_DEV void fixed_fields(const uint8_t *s_win, int64_t abase, int64_t x, int32_t f[8]) {
-  const int r = (int)(x - abase);
-  const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win) + (r >> 2);
-  const int o = r & 3;
-  uint32_t W[9];
-#pragma unroll
-  for (int j = 0; j < 9; j++) W[j] = w32[j];
-#pragma unroll
-  for (int j = 0; j < 8; j++) f[j] = (int32_t)__builtin_amdgcn_alignbyte(W[j + 1], W[j], o);
-}
-
-enum { MODE_COUNTS = 0, MODE_EAGER = 1, MODE_WORDS = 2 };
-
-template <int MODE>
-__global__ __launch_bounds__(kCheckThreads) void k_check(StreamView sv, int64_t x0, int64_t x1, int R, CountsDev cd,
-                                                         unsigned long long *__restrict__ bitmap,
-                                                         uint32_t *__restrict__ words) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_win[kWin + 16];
-  __shared__ uint32_t s_cnt[21 * 19];
-  __shared__ uint32_t s_npos[21];
-  const int lane = lane_id();
-  if (MODE == MODE_COUNTS) {
-    for (int i = threadIdx.x; i < 21 * 19; i += kCheckThreads) s_cnt[i] = 0;
-    if (threadIdx.x < 21) s_npos[threadIdx.x] = 0;
-  }
-  unsigned long long n_succ = 0, n_tff = 0, n_halo = 0;  // lane 0 of each wave accumulates
-  const int64_t ntiles = (x1 - x0 + kTile - 1) / kTile;
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-    const int64_t base = x0 + t * kTile;
-    const int64_t abase = base & ~(int64_t)15;
-    __syncthreads();
-    stage(s_win, sv.u, abase);
-    __syncthreads();
-    const Win w{s_win, abase, kWin, sv.u};
-    for (int j = 0; j < kTile / kCheckThreads; j++) {
-      const int64_t x = base + j * kCheckThreads + threadIdx.x;
-      const bool valid = x < x1;
-      uint32_t word = 0;
-      if (valid) {
-        int32_t f[8];
-        fixed_fields(s_win, abase, x, f);
-        word = check_from<MODE == MODE_EAGER>(w, sv, x, R, f);
-      }
-      if (MODE == MODE_WORDS) {
-        if (valid) words[x - x0] = word;
-        continue;
-      }
-      const bool succ = valid && (word & W_SUCC);
-      const unsigned long long sm = __ballot(succ);
-      const int64_t rel = base - x0 + j * kCheckThreads + (threadIdx.x & ~63);
-      if (lane == 0 && bitmap) bitmap[rel >> 6] = sm;
-      if (MODE == MODE_COUNTS) {
-        const bool halo = valid && word == W_HALO;
-        const bool tff = valid && word == 1u;
-        const bool counted = valid && !succ && !halo && !tff;
-        const unsigned long long hm = __ballot(halo), tm = __ballot(tff);
-        if (lane == 0) {
-          n_succ += __popcll(sm);
-          n_tff += __popcll(tm);
-          n_halo += __popcll(hm);
-        }
-        const uint32_t F = word & 0x7ffffu;
-        const uint32_t kk = (word >> 24) & 0x7fu;
-        const uint32_t key = (uint32_t)__popc(F) + (kk > 0 ? 1u : 0u);
-        uint32_t present = wave_or(counted ? (1u << key) : 0u);
-        while (present) {
-          const uint32_t k = __builtin_ctz(present);
-          present &= present - 1;
-          const bool in = counted && key == k;
-          const unsigned long long km = __ballot(in);
-          uint32_t mycnt = 0;
-#pragma unroll
-          for (int f = 0; f < 19; f++) {
-            const unsigned long long m = __ballot(in && ((F >> f) & 1u));
-            mycnt = (lane == f) ? (uint32_t)__popcll(m) : mycnt;
-          }
-          if (lane < 19 && mycnt) atomicAdd(&s_cnt[k * 19 + lane], mycnt);
-          if (lane == 19) atomicAdd(&s_npos[k], (uint32_t)__popcll(km));
-        }
-        if (counted && kk > 0) atomicAdd(&cd.rbe[key * 128 + kk], 1ull);
-        if (counted && key == 2) {  // close calls: histogram of the two failing flags
-          const uint32_t fi = __builtin_ctz(F);
-          const uint32_t rest = F & (F - 1);
-          const uint32_t fj = rest ? __builtin_ctz(rest) : fi;  // k>0 with one flag: (fi, fi)
-          atomicAdd(&cd.pair[fi * 19 + fj], 1ull);
-        }
-      }
-    }
-  }
-  if (MODE == MODE_COUNTS) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < 21 * 19; i += kCheckThreads)
-      if (s_cnt[i]) atomicAdd(&cd.counts[i], (unsigned long long)s_cnt[i]);
-    if (threadIdx.x < 21 && s_npos[threadIdx.x]) atomicAdd(&cd.positions[threadIdx.x], (unsigned long long)s_npos[threadIdx.x]);
-    if (lane == 0) {
-      if (n_succ) atomicAdd(&cd.scalars[1], n_succ);
-      if (n_tff) atomicAdd(&cd.scalars[2], n_tff);
-      if (n_halo) atomicAdd(&cd.scalars[3], n_halo);
-    }
-  }
-}
-
-// FindRecordStart.withDelta for a batch of start offsets: one workgroup per start scans 256 positions per
-// step (eager checker, global reads) until the first true call; with a success bitmap covering [bx0, bx1)
-// the covered prefix is read from the bitmap instead.  out = found offset, -1 = None, -2 = HALO.
-__global__ __launch_bounds__(kCheckThreads) void k_find_record_starts(StreamView sv, const int64_t *__restrict__ xs,
-                                                                      int R, int64_t max_read_size,
-                                                                      const unsigned long long *__restrict__ bitmap,
-                                                                      int64_t bx0, int64_t bx1,
-                                                                      int64_t *__restrict__ out) {
-  __shared__ unsigned long long s_best;
-  __shared__ int s_halo;
-  const int64_t x0 = xs[blockIdx.x];
-  if (threadIdx.x == 0) { s_best = ~0ull; s_halo = 0; }
-  __syncthreads();
-  if (x0 < 0) { if (threadIdx.x == 0) out[blockIdx.x] = -1; return; }
-  const int64_t lim = min(sv.L, x0 + max_read_size);
-  int64_t x = x0;
-  if (bitmap && x0 >= bx0 && x0 < bx1) {
-    const int64_t blim = min(lim, bx1);
-    for (int64_t wb = (x0 - bx0) >> 6; bx0 + (wb << 6) < blim; wb += kCheckThreads) {
-      const int64_t wi = wb + threadIdx.x;
-      const int64_t wx = bx0 + (wi << 6);
-      if (wx < blim) {
-        unsigned long long m = bitmap[wi];
-        if (wx < x0) m &= ~0ull << (x0 - wx);
-        if (m) {
-          const int64_t hit = wx + __ffsll((long long)m) - 1;
-          if (hit < blim) atomicMin(&s_best, (unsigned long long)hit);
-        }
-      }
-      __syncthreads();
-      if (s_best != ~0ull) break;
-      __syncthreads();
-    }
-    x = blim;
-  }
-  const Win w{nullptr, 0, 0, sv.u};
-  while (s_best == ~0ull && x < lim && !s_halo) {
-    const int64_t p = x + threadIdx.x;
-    if (p < lim) {
-      int32_t f[8];
-      if (p + 36 <= sv.L) {
-#pragma unroll
-        for (int j = 0; j < 8; j++) f[j] = w.i32(p + 4 * j);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; j++) f[j] = 0;
-      }
-      const uint32_t word = check_from<true>(w, sv, p, R, f);
-      if (word == W_HALO) s_halo = 1;
-      else if (word & W_SUCC) atomicMin(&s_best, (unsigned long long)p);
-    }
-    __syncthreads();
-    x += kCheckThreads;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) out[blockIdx.x] = (s_best != ~0ull) ? (int64_t)s_best : (s_halo ? -2 : -1);
-}
-
-SB_DEV int32_t g_i32(const uint8_t *u, int64_t x) {
-  return (int32_t)((uint32_t)u[x] | ((uint32_t)u[x + 1] << 8) | ((uint32_t)u[x + 2] << 16) | ((uint32_t)u[x + 3] << 24));
-}
-
-// Record chain per split (RecordStream._advance / PosStream): r_{j+1} = r_j + 4 + block_size while r_j < x_end.
-// counts[i] = records, or -2 when the chain left a shard's loaded bytes (HALO), -3 on a truncated record.
-__global__ void k_record_counts(StreamView sv, const int64_t *__restrict__ xs, const int64_t *__restrict__ xe, int64_t n,
-                                int64_t *__restrict__ counts) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  int64_t x = xs[i];
-  const int64_t end = xe[i];
-  int64_t c = 0;
-  if (x >= 0) {
-    while (x < end) {
-      if (x + 4 > sv.L) { c = sv.eof_real ? -3 : -2; break; }
-      const int32_t bs = g_i32(sv.u, x);
-      if (bs < 0 || x + 4 + (int64_t)bs > sv.L) { c = sv.eof_real ? -3 : -2; break; }
-      c++;
-      x += 4 + (int64_t)bs;
-    }
-  }
-  counts[i] = c;
-}
-
-__global__ void k_record_offsets(StreamView sv, int64_t x, int64_t end, int64_t *__restrict__ offs, int64_t cap,
-                                 int64_t *__restrict__ n_out) {
-  int64_t c = 0;
-  while (x < end) {
-    if (x + 4 > sv.L) { c = -3 - c; break; }
-    const int32_t bs = g_i32(sv.u, x);
-    if (bs < 0 || x + 4 + (int64_t)bs > sv.L) { c = -3 - c; break; }
-    if (c < cap) offs[c] = x;
-    c++;
-    x += 4 + (int64_t)bs;
-  }
-  *n_out = c;
-}
-
-// ================================================================================================
 // launch wrappers
 // ================================================================================================
-static int check_grid(int64_t ntiles) { return (int)(ntiles < 1 ? 1 : ntiles > 2048 ? 2048 : ntiles); }
 
 hipError_t launch_scan_count(const uint8_t *d, int64_t D, int32_t *cc, int64_t nchunks, hipStream_t s) {
   if (nchunks == 0) return hipSuccess;
@@ -963,47 +627,4 @@ hipError_t launch_inflate(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *o
                      next_block, first_err);
   return hipGetLastError();
 }
-hipError_t launch_check_full_counts(StreamView sv, int64_t x0, int64_t x1, int32_t R, CountsDev cd,
-                                    unsigned long long *bitmap, hipStream_t s) {
-  if (x1 <= x0) return hipSuccess;
-  const int64_t nt = (x1 - x0 + kTile - 1) / kTile;
-  hipLaunchKernelGGL(k_check<MODE_COUNTS>, dim3(check_grid(nt)), dim3(kCheckThreads), 0, s, sv, x0, x1, R, cd, bitmap,
-                     nullptr);
-  return hipGetLastError();
-}
-hipError_t launch_check_eager(StreamView sv, int64_t x0, int64_t x1, int32_t R, unsigned long long *bitmap,
-                              hipStream_t s) {
-  if (x1 <= x0) return hipSuccess;
-  const int64_t nt = (x1 - x0 + kTile - 1) / kTile;
-  hipLaunchKernelGGL(k_check<MODE_EAGER>, dim3(check_grid(nt)), dim3(kCheckThreads), 0, s, sv, x0, x1, R, CountsDev{},
-                     bitmap, nullptr);
-  return hipGetLastError();
-}
-hipError_t launch_check_words(StreamView sv, int64_t x0, int64_t x1, int32_t R, uint32_t *words, hipStream_t s) {
-  if (x1 <= x0) return hipSuccess;
-  const int64_t nt = (x1 - x0 + kTile - 1) / kTile;
-  hipLaunchKernelGGL(k_check<MODE_WORDS>, dim3(check_grid(nt)), dim3(kCheckThreads), 0, s, sv, x0, x1, R, CountsDev{},
-                     nullptr, words);
-  return hipGetLastError();
-}
-hipError_t launch_find_record_starts(StreamView sv, const int64_t *x0, int64_t n, int32_t R, int64_t mrs,
-                                     const unsigned long long *bitmap, int64_t bx0, int64_t bx1, int64_t *out,
-                                     hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_find_record_starts, dim3((unsigned)n), dim3(kCheckThreads), 0, s, sv, x0, R, mrs, bitmap, bx0,
-                     bx1, out);
-  return hipGetLastError();
-}
-hipError_t launch_record_counts(StreamView sv, const int64_t *x0, const int64_t *xe, int64_t n, int64_t *counts,
-                                hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_record_counts, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, sv, x0, xe, n, counts);
-  return hipGetLastError();
-}
-hipError_t launch_record_offsets(StreamView sv, int64_t x0, int64_t xe, int64_t *offs, int64_t cap, int64_t *n_out,
-                                 hipStream_t s) {
-  hipLaunchKernelGGL(k_record_offsets, dim3(1), dim3(1), 0, s, sv, x0, xe, offs, cap, n_out);
-  return hipGetLastError();
-}
-
 }  // namespace sbam

@@ -1,0 +1,765 @@
+// sbam_check.hip — record-boundary checker, FindRecordStart scan and record-chain walk (gfx950).
+//
+//  * full.Checker / eager.Checker at every uncompressed offset
+//      (check/.../check/full/Checker.scala:22-184, eager/Checker.scala:24-126, PosChecker.scala:43-63)
+//  * full-check Counts reduction (check/.../full/error/Counts.scala; cli/.../full/FullCheck.scala:141-191)
+//  * FindRecordStart.withDelta (check/.../bam/spark/FindRecordStart.scala:30-63)
+//  * RecordStream / PosStream chain (check/.../bam/iterator/RecordStream.scala:27-41)
+//
+// Layout: a workgroup stages a tile of the uncompressed stream (8 KiB of positions + a
+// 768-B halo) in LDS and, while staging, builds an LDS bitmap of "CIGAR op invalid at this byte"
+// ((b & 0xf) > 8 — an op's validity depends only on its first byte).  Each lane then evaluates FOUR
+// consecutive positions from ten shared LDS dwords (v_alignbyte per offset).  The first record of a
+// position is checked against the window; a CIGAR scan is a masked ctz over the bitmap (16 ops per 64-bit
+// word) instead of a per-lane loop whose wave cost is the slowest lane; read names are checked 4 bytes at a
+// time (SWAR).  Positions whose first record passes (true starts and rare near-misses) continue the
+// 10-record chain from global memory.  Counts are accumulated per lane in carry-save bit planes (19 flags)
+// and packed 8-bit key counters, reduced with ballots once per 7 tiles.
+#include "sbam_internal.h"
+
+#ifndef SBAM_ABLATE
+#define SBAM_ABLATE 0
+#endif
+
+namespace sbam {
+
+#define SB_DEV __device__ __forceinline__
+
+constexpr uint32_t W_SUCC = 0x80000000u, W_HALO = 0x00800000u;
+constexpr uint32_t W_PASS0 = 0x40000000u;  // internal: first record passed, chain pending
+constexpr uint32_t W_NONE = 0xffffffffu;   // internal: position outside [x0, x1)
+constexpr int kCheckThreads = 256;
+constexpr int kTile = 8192;                 // positions per tile (64-aligned tile bases)
+constexpr int kHalo = 768;                  // staged bytes past the tile (fixed fields + 255-B name + ops)
+constexpr int kWin = kTile + kHalo;         // staged window (multiple of 16)
+constexpr int kInvWords = kWin / 32 + 4;    // bitmap words (+ pad for 64-bit extraction)
+constexpr int kLdsLens = 4096;              // contig lengths kept in LDS when n_ref fits
+constexpr int kFlushTiles = 7;              // 7 tiles x 32 positions per lane < 255 (8-bit planes / counters)
+static_assert(kWin % 16 == 0, "window");
+
+SB_DEV int lane_id() { return __lane_id(); }
+
+SB_DEV uint64_t shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = __shfl_xor((int)(uint32_t)v, m, 64), hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+SB_DEV uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor((int)v, o, 64);
+  return v;
+}
+SB_DEV uint32_t wave_or(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v |= __shfl_xor((int)v, o, 64);
+  return v;
+}
+
+// ---- byte-class SWAR ---------------------------------------------------------------------------
+// 4 bits: (byte j of w) & 0xf > 8  (Checker.MAX_CIGAR_OP = 8, check/.../check/Checker.scala:21)
+SB_DEV uint32_t inv_nibble(uint32_t w) {
+  const uint32_t t = (((w & 0x0f0f0f0fu) + 0x07070707u) >> 4) & 0x01010101u;
+  return ((t * 0x00204081u) >> 21) & 0xfu;
+}
+// bytes outside allowedReadNameChars = ('!' to '?') ++ ('A' to '~') (Checker.scala:12-17), bit 7 of each byte
+SB_DEV uint32_t name_bad_bytes(uint32_t w) {
+  const uint32_t hi = w & 0x80808080u, lo7 = w & 0x7f7f7f7fu;
+  const uint32_t lt33 = ~(lo7 + 0x5f5f5f5fu) & 0x80808080u;
+  const uint32_t eq127 = (lo7 + 0x01010101u) & 0x80808080u;
+  const uint32_t z = lo7 ^ 0x40404040u;
+  const uint32_t eq64 = ~((z + 0x7f7f7f7fu) | z) & 0x80808080u;
+  return hi | lt33 | eq127 | eq64;
+}
+
+SB_DEV int32_t g_i32(const uint8_t *u, int64_t x) {
+  return (int32_t)((uint32_t)u[x] | ((uint32_t)u[x + 1] << 8) | ((uint32_t)u[x + 2] << 16) | ((uint32_t)u[x + 3] << 24));
+}
+
+// PosChecker.getRefPosError as bits {negIdx, bigIdx, negPos, bigPos}.  negPos = refPos < -1 in every branch;
+// bigPos only when 0 <= refIdx < n_ref and refPos > len[refIdx] (note '>': refPos == len passes).
+SB_DEV uint32_t ref_err(int32_t ri, int32_t rp, const int32_t *lensL, const int64_t *lensG, int32_t nref) {
+  uint32_t f = (ri < -1) ? 1u : 0u;
+  f |= (ri >= nref) ? 2u : 0u;
+  f |= (rp < -1) ? 4u : 0u;
+  if ((uint32_t)ri < (uint32_t)nref && rp > 0) {
+    const int64_t len = lensL ? (int64_t)lensL[ri] : lensG[ri];
+    f |= ((int64_t)rp > len) ? 8u : 0u;
+  }
+  return f;
+}
+
+// (l_seq + 1) / 2 + l_seq and 32 + l_read_name + 4 n_cigar + that, in Java Int (wrap, '/' toward zero)
+SB_DEV bool too_few_remaining(int32_t bs, int32_t lrn, int32_t nc, int32_t ls) {
+  const int32_t t = (int32_t)((uint32_t)ls + 1u);
+  const int32_t nsq = (int32_t)((uint32_t)(t / 2) + (uint32_t)ls);
+  const int32_t implied = (int32_t)(32u + (uint32_t)lrn + 4u * (uint32_t)nc + (uint32_t)nsq);
+  return bs < implied;
+}
+
+// ---- generic chain (global memory): records k, k+1, ... from logical start s, read cursor a -----------------
+// full/Checker.scala:22-184 line by line; EAGER stops at the first failing group (boolean identical).
+struct GlobalBytes {
+  const uint8_t *u;
+  SB_DEV uint32_t operator()(int64_t x) const { return u[x]; }
+};
+
+template <bool EAGER, class Bytes>
+SB_DEV uint32_t check_chain(const StreamView &sv, const Bytes &u, int64_t s, int64_t a, int k, int R) {
+  auto g_i32 = [&](const Bytes &b, int64_t x) -> int32_t {
+    return (int32_t)(b(x) | (b(x + 1) << 8) | (b(x + 2) << 16) | (b(x + 3) << 24));
+  };
+  for (;;) {
+    if (k == R) return W_SUCC | ((uint32_t)k << 24);
+    if (a + 36 > sv.L) {
+      if (!sv.eof_real) return W_HALO;
+      if (k > 0 && s == sv.L) return W_SUCC | ((uint32_t)k << 24);
+      return 1u | ((uint32_t)k << 24);
+    }
+    const int32_t bs = g_i32(u, a), ri = g_i32(u, a + 4), rp = g_i32(u, a + 8), bmn = g_i32(u, a + 12);
+    const int32_t fnc = g_i32(u, a + 16), ls = g_i32(u, a + 20), nri = g_i32(u, a + 24), nrp = g_i32(u, a + 28);
+    const uint32_t K = (uint32_t)k << 24;
+    uint32_t F = ref_err(ri, rp, nullptr, sv.lens, sv.nref) << 1;
+    const int32_t lrn = bmn & 0xff;
+    const uint32_t flag = ((uint32_t)fnc) >> 16;
+    const int32_t nc = fnc & 0xffff;
+    F |= too_few_remaining(bs, lrn, nc, ls) ? (1u << 18) : 0u;
+    F |= ref_err(nri, nrp, nullptr, sv.lens, sv.nref) << 5;
+    if (EAGER && (F || lrn < 2 || ((flag & 4u) == 0 && (ls == 0 || nc == 0)))) return K | (F ? F : (1u << 12));
+    int64_t c = a + 36;
+    if (lrn == 0) {
+      F |= 1u << 12;
+    } else if (lrn == 1) {
+      F |= 1u << 13;
+    } else {
+      if (c + lrn > sv.L) {
+        if (!sv.eof_real) return W_HALO;
+        return K | F | (1u << 9);
+      }
+      if (u(c + lrn - 1) != 0) {
+        F |= 1u << 10;
+      } else {
+        for (int32_t i = 0; i < lrn - 1; i++) {
+          const uint32_t b = u(c + i);
+          if (!((b - 33u <= 30u) || (b - 65u <= 61u))) { F |= 1u << 11; break; }
+        }
+      }
+      c += lrn;
+      if (EAGER && F) return K | F;
+    }
+    bool cig_err = false;
+    for (int32_t i = 0; i < nc; i++) {
+      if (c + 4 > sv.L) {
+        if (!sv.eof_real) return W_HALO;
+        F |= 1u << 14;
+        cig_err = true;
+        break;
+      }
+      const uint32_t op = u(c);
+      c += 4;
+      if ((op & 0xfu) > 8u) { F |= 1u << 15; cig_err = true; break; }
+    }
+    if (!cig_err && (flag & 4u) == 0 && (ls == 0 || nc == 0)) {
+      F |= (ls == 0) ? (1u << 16) : 0u;  // EmptyMapped(emptySeq, emptyCigar) → (emptyMappedCigar, emptyMappedSeq)
+      F |= (nc == 0) ? (1u << 17) : 0u;
+    }
+    if (F) return K | F;
+    const int64_t nxt = s + 4 + (int64_t)bs;
+    if (nxt > c) {
+      if (nxt > sv.L && !sv.eof_real) return W_HALO;
+      a = nxt > sv.L ? sv.L : nxt;  // skip past EOF clamps (parity unpinned: SURVEY §8(c))
+    } else {
+      a = c;
+    }
+    s = nxt;
+    k++;
+  }
+}
+
+// ---- chain pass ----------------------------------------------------------------------------------------------
+// k_check leaves, for every position of [x0, x1), a bit meaning "the record read at this position passes every
+// check" (PASS0).  A position's call is Success iff the first R records of its chain pass, so k_chains walks
+// the chain of each PASS0 position: a record whose start is itself a PASS0 position is already known to pass
+// (one bit read + 12 bytes to find the next record); any other record is checked in full from global memory.
+// A failing chain clears its bit, so the bitmap becomes the success bitmap; bits are only a shortcut (a
+// cleared bit is re-checked in full), so concurrent clears never change a result.
+SB_DEV uint32_t walk_chain(const StreamView &sv, const unsigned long long *bitmap, int64_t x0a, int64_t x1, int64_t p,
+                           int R) {
+  int64_t s = p, a = p;
+  int k = 0;
+  for (;;) {
+    if (k == R) return W_SUCC | ((uint32_t)k << 24);
+    if (a + 36 > sv.L) {
+      if (!sv.eof_real) return W_HALO;
+      if (k > 0 && s == sv.L) return W_SUCC | ((uint32_t)k << 24);
+      return 1u | ((uint32_t)k << 24);
+    }
+    const int32_t bs = g_i32(sv.u, a);
+    int64_t c_end;
+    const int64_t r = a - x0a;
+    const bool fast = a == s && a < x1 && r >= 0 && ((bitmap[r >> 6] >> (r & 63)) & 1ull);
+    if (fast) {
+      const int32_t lrn = sv.u[a + 12];
+      const int32_t nc = (int32_t)((uint32_t)sv.u[a + 16] | ((uint32_t)sv.u[a + 17] << 8));
+      c_end = a + 36 + (lrn >= 2 ? lrn : 0) + 4 * (int64_t)nc;
+    } else {
+      // full check of this record: the generic chain restricted to one record (k fixed, R = k + 1)
+      const uint32_t w = check_chain<false>(sv, GlobalBytes{sv.u}, s, a, k, k + 1);
+      if (w == W_HALO || !(w & W_SUCC)) return w;
+      const int32_t lrn = sv.u[a + 12];
+      const int32_t nc = (int32_t)((uint32_t)sv.u[a + 16] | ((uint32_t)sv.u[a + 17] << 8));
+      c_end = a + 36 + (lrn >= 2 ? lrn : 0) + 4 * (int64_t)nc;
+    }
+    const int64_t nxt = s + 4 + (int64_t)bs;
+    if (nxt > c_end) {
+      if (nxt > sv.L && !sv.eof_real) return W_HALO;
+      a = nxt > sv.L ? sv.L : nxt;
+    } else {
+      a = c_end;
+    }
+    s = nxt;
+    k++;
+  }
+}
+
+SB_DEV void count_chain_result(const CountsDev &cd, uint32_t w, bool bykey) {
+  if (w == W_HALO) { atomicAdd(&cd.scalars[3], 1ull); return; }
+  if (w & W_SUCC) return;
+  const uint32_t F = w & 0x7ffffu, kk = (w >> 24) & 0x7fu;
+  if (F == 1u && kk == 0) { atomicAdd(&cd.scalars[2], 1ull); return; }
+  const uint32_t key = (uint32_t)__popc(F) + (kk > 0 ? 1u : 0u);
+  atomicAdd(&cd.positions[key], 1ull);
+  for (uint32_t m = F; m; m &= m - 1) {
+    const uint32_t f = __builtin_ctz(m);
+    atomicAdd(&cd.totals[f], 1ull);
+    if (bykey || key <= 2) atomicAdd(&cd.counts[key * 19 + f], 1ull);
+  }
+  if (key == 2) {
+    const uint32_t fi = __builtin_ctz(F), rest = F & (F - 1);
+    atomicAdd(&cd.pair[fi * 19 + (rest ? __builtin_ctz(rest) : fi)], 1ull);
+  }
+  if (kk > 0) atomicAdd(&cd.rbe[key * 128 + kk], 1ull);
+}
+
+// One lane per bitmap word; cd.counts == nullptr skips counting (eager), words != nullptr writes results.
+__global__ __launch_bounds__(256) void k_chains(StreamView sv, int64_t x0, int64_t x1, int R,
+                                                unsigned long long *__restrict__ bitmap, CountsDev cd, int bykey,
+                                                uint32_t *__restrict__ words) {
+  const int64_t x0a = x0 & ~(int64_t)63;
+  const int64_t nwords = (x1 - x0a + 63) >> 6;
+  uint32_t n_succ = 0;
+  for (int64_t wi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; wi < nwords; wi += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long m = bitmap[wi];
+    if (!m) continue;
+    unsigned long long keep = m;
+    for (unsigned long long q = m; q; q &= q - 1) {
+      const int b = __builtin_ctzll(q);
+      const int64_t p = x0a + 64 * wi + b;
+      const uint32_t w = walk_chain(sv, bitmap, x0a, x1, p, R);
+      if (w & W_SUCC) n_succ++;
+      else keep &= ~(1ull << b);
+      if (cd.counts) count_chain_result(cd, w, bykey != 0);
+      if (words) words[p - x0] = w;
+    }
+    if (keep != m) bitmap[wi] = keep;
+  }
+  if (cd.counts) {
+    for (int o = 32; o >= 1; o >>= 1) n_succ += __shfl_xor((int)n_succ, o, 64);
+    if (lane_id() == 0 && n_succ) atomicAdd(&cd.scalars[1], (unsigned long long)n_succ);
+  }
+}
+
+// ---- first record against the LDS window --------------------------------------------------------------------
+struct Tile {
+  const uint8_t *win;   // staged bytes: win[r] = u[base + r], r < kWin
+  const uint32_t *inv;  // bit r: (win[r] & 0xf) > 8
+  int64_t base;
+};
+
+SB_DEV uint32_t byte_at(const Tile &t, const StreamView &sv, int64_t x) {
+  const int64_t r = x - t.base;
+  return r < kWin ? (uint32_t)t.win[r] : (uint32_t)sv.u[x];
+}
+struct TileBytes {  // the staged window where it covers x, else global memory
+  const uint8_t *win;
+  int64_t base;
+  const uint8_t *u;
+  SB_DEV uint32_t operator()(int64_t x) const {
+    const int64_t r = x - base;
+    return r < kWin ? (uint32_t)win[r] : (uint32_t)u[x];
+  }
+};
+
+SB_DEV uint64_t bits64(const uint32_t *bm, int x) {
+  const int w = x >> 5, s = x & 31;
+  const uint64_t lo = (uint64_t)bm[w] | ((uint64_t)bm[w + 1] << 32);
+  const uint64_t hi = bm[w + 2];
+  return s ? (lo >> s) | (hi << (64 - s)) : lo;
+}
+
+// Any byte of [c, c+n) outside allowedReadNameChars?  SWAR over aligned window dwords.
+SB_DEV bool name_has_bad(const Tile &t, const StreamView &sv, int64_t c, int32_t n) {
+  if (n <= 0) return false;
+  const int64_t rel = c - t.base;
+  if (rel + n <= kWin) {
+    const uint32_t *w32 = reinterpret_cast<const uint32_t *>(t.win);
+    const int r0 = (int)rel, r1 = (int)rel + n;
+    for (int d = r0 & ~3; d < r1; d += 4) {
+      uint32_t w = w32[d >> 2];
+      const int lo = r0 > d ? r0 - d : 0, hi = r1 - d < 4 ? r1 - d : 4;
+      const uint32_t keep = (uint32_t)((0xffffffffull << (8 * lo)) & ((1ull << (8 * hi)) - 1));
+      w = (w & keep) | (0x41414141u & ~keep);
+      if (name_bad_bytes(w)) return true;
+    }
+    return false;
+  }
+  for (int32_t i = 0; i < n; i++) {
+    const uint32_t b = sv.u[c + i];
+    if (!((b - 33u <= 30u) || (b - 65u <= 61u))) return true;
+  }
+  return false;
+}
+
+// Index of the first op among the first `lim` ops at c, c+4, ... whose first byte has (b & 0xf) > 8, or lim.
+SB_DEV int32_t first_bad_op(const Tile &t, const StreamView &sv, int64_t c, int32_t lim) {
+  const int64_t rel = c - t.base;
+  const int32_t nwin = rel < kWin ? (int32_t)((kWin - rel + 3) >> 2) : 0;
+  const int32_t n1 = lim < nwin ? lim : nwin;
+  for (int32_t i = 0; i < n1; i += 16) {
+    uint64_t m = bits64(t.inv, (int)rel + 4 * i) & 0x1111111111111111ull;
+    const int32_t rem = n1 - i;
+    if (rem < 16) m &= (1ull << (4 * rem)) - 1ull;
+    if (m) return i + (int32_t)(__builtin_ctzll(m) >> 2);
+  }
+  for (int32_t i = n1; i < lim; i++)
+    if ((sv.u[c + 4 * (int64_t)i] & 0xfu) > 8u) return i;
+  return lim;
+}
+
+template <bool EAGER>
+SB_DEV uint32_t check_first(const Tile &t, const StreamView &sv, const int32_t *lensL, int64_t x, int R,
+                            const int32_t f[8]) {
+  if (R == 0) return W_PASS0;  // Success(0): resolved by the chain pass
+  if (x + 36 > sv.L) return sv.eof_real ? 1u : W_HALO;
+  const int32_t bs = f[0], ri = f[1], rp = f[2], bmn = f[3], fnc = f[4], ls = f[5], nri = f[6], nrp = f[7];
+  uint32_t F = ref_err(ri, rp, lensL, sv.lens, sv.nref) << 1;
+  const int32_t lrn = bmn & 0xff;
+  const uint32_t flag = ((uint32_t)fnc) >> 16;
+  const int32_t nc = fnc & 0xffff;
+  F |= too_few_remaining(bs, lrn, nc, ls) ? (1u << 18) : 0u;
+  F |= ref_err(nri, nrp, lensL, sv.lens, sv.nref) << 5;
+  const bool empty_mapped = (flag & 4u) == 0 && (ls == 0 || nc == 0);
+  if (EAGER && (F || lrn < 2 || empty_mapped)) return F ? F : (1u << 12);
+#if SBAM_ABLATE == 1  // timing experiment only: fixed-field checks alone
+  return F | (1u << 15);
+#endif
+  int64_t c = x + 36;
+  if (lrn < 2) {
+    F |= lrn == 0 ? (1u << 12) : (1u << 13);
+  } else {
+    if (c + lrn > sv.L) return sv.eof_real ? (F | (1u << 9)) : W_HALO;
+    if (byte_at(t, sv, c + lrn - 1) != 0) F |= 1u << 10;
+    else if (name_has_bad(t, sv, c, lrn - 1)) F |= 1u << 11;
+    c += lrn;
+    if (EAGER && F) return F;
+  }
+  bool cig_err = false;
+#if SBAM_ABLATE == 2  // timing experiment only: no CIGAR scan
+  return F | (1u << 15);
+#endif
+  if (nc > 0) {
+    const int64_t n_eof = (sv.L - c) >> 2;  // ops readable before EOF (c <= L here)
+    const int32_t lim = n_eof < nc ? (int32_t)n_eof : nc;
+    const int32_t bad = first_bad_op(t, sv, c, lim);
+    if (bad < lim) {
+      F |= 1u << 15;
+      cig_err = true;
+    } else if (n_eof < nc) {
+      if (!sv.eof_real) return W_HALO;
+      F |= 1u << 14;
+      cig_err = true;
+    }
+  }
+  if (!cig_err && empty_mapped) {
+    F |= (ls == 0) ? (1u << 16) : 0u;
+    F |= (nc == 0) ? (1u << 17) : 0u;
+  }
+  if (F) return F;
+  // record 0 passed (true starts and rare near-misses): the 10-record chain is resolved after the tile's
+  // positions, one candidate per lane, so it never stalls a whole wave-step (k_check, deferred pass)
+  return W_PASS0;
+}
+
+// ---- the tiled kernel -------------------------------------------------------------------------------------
+enum { MODE_COUNTS = 0, MODE_EAGER = 1, MODE_WORDS = 2, MODE_BYKEY = 3 };
+
+struct Planes {  // carry-save bit planes: per-flag counts of up to 255 values per lane
+  uint32_t p[8];
+  SB_DEV void clear() {
+#pragma unroll
+    for (int j = 0; j < 8; j++) p[j] = 0;
+  }
+  // add a 3-plane number (o1 weight 1, o2 weight 2, o4 weight 4)
+  SB_DEV void add(uint32_t o1, uint32_t o2, uint32_t o4) {
+    uint32_t c = p[0] & o1;
+    p[0] ^= o1;
+    uint32_t s = p[1] ^ o2 ^ c;
+    c = (p[1] & o2) | (c & (p[1] ^ o2));
+    p[1] = s;
+    s = p[2] ^ o4 ^ c;
+    c = (p[2] & o4) | (c & (p[2] ^ o4));
+    p[2] = s;
+#pragma unroll
+    for (int j = 3; j < 8; j++) {
+      const uint32_t t = p[j] & c;
+      p[j] ^= c;
+      c = t;
+    }
+  }
+};
+
+// Count one checked position into the lane's accumulators (full-check Counts semantics).
+struct Acc {
+  Planes pl;
+  uint64_t keyc[3];  // 8-bit counters per key (8 per word)
+  uint32_t n_succ, n_tff, n_halo;
+  SB_DEV void clear() {
+    pl.clear();
+    keyc[0] = keyc[1] = keyc[2] = 0;
+    n_succ = n_tff = n_halo = 0;
+  }
+  // classify w; returns the counted flag word F (0 if not counted); rare per-key paths go to global atomics
+  template <bool BYKEY>
+  SB_DEV uint32_t classify(uint32_t w, const CountsDev &cd, uint32_t &key_out, bool &counted_out) {
+    const bool succ = (w & W_SUCC) != 0;
+    const bool halo = w == W_HALO;
+    const bool tff = w == 1u;
+    const bool counted = !succ && !halo && !tff;
+    n_succ += succ;
+    n_halo += halo;
+    n_tff += tff;
+    const uint32_t F = counted ? (w & 0x7ffffu) : 0u;
+    const uint32_t kk = (w >> 24) & 0x7fu;
+    const uint32_t key = (uint32_t)__popc(F) + (kk > 0 ? 1u : 0u);
+    if (counted) {
+      const uint64_t inc = 1ull << (8 * (key & 7));
+      keyc[0] += (key >> 3) == 0 ? inc : 0ull;
+      keyc[1] += (key >> 3) == 1 ? inc : 0ull;
+      keyc[2] += (key >> 3) == 2 ? inc : 0ull;
+      if (key <= 2 || kk > 0) {  // rare: keys 1-2 per flag, close-call pairs, readsBeforeError histogram
+        if (!BYKEY && key <= 2)
+          for (uint32_t m = F; m; m &= m - 1) atomicAdd(&cd.counts[key * 19 + __builtin_ctz(m)], 1ull);
+        if (key == 2) {
+          const uint32_t fi = __builtin_ctz(F), rest = F & (F - 1);
+          atomicAdd(&cd.pair[fi * 19 + (rest ? __builtin_ctz(rest) : fi)], 1ull);
+        }
+        if (kk > 0) atomicAdd(&cd.rbe[key * 128 + kk], 1ull);
+      }
+    }
+    key_out = key;
+    counted_out = counted;
+    return F;
+  }
+};
+
+// Reduce the lanes' accumulators into the workgroup's LDS totals (ballots over bit planes; wave sums).
+SB_DEV void flush_acc(Acc &acc, unsigned long long *s_acc, int lane) {
+#pragma unroll
+  for (int f = 0; f < 19; f++) {
+    uint32_t tot = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) tot += (uint32_t)__popcll(__ballot((acc.pl.p[j] >> f) & 1u)) << j;
+    if (lane == 0 && tot) atomicAdd(&s_acc[f], (unsigned long long)tot);
+  }
+#pragma unroll
+  for (int k = 0; k < 21; k++) {
+    const uint32_t v = wave_sum((uint32_t)(acc.keyc[k >> 3] >> (8 * (k & 7))) & 0xffu);
+    if (lane == 0 && v) atomicAdd(&s_acc[19 + k], (unsigned long long)v);
+  }
+  const uint32_t a = wave_sum(acc.n_succ), b = wave_sum(acc.n_tff), h = wave_sum(acc.n_halo);
+  if (lane == 0) {
+    if (a) atomicAdd(&s_acc[40], (unsigned long long)a);
+    if (b) atomicAdd(&s_acc[41], (unsigned long long)b);
+    if (h) atomicAdd(&s_acc[42], (unsigned long long)h);
+  }
+  acc.clear();
+}
+
+// Exact per-key flag counts (MODE_BYKEY): 19 ballots per key present in the wave.
+SB_DEV void bykey_count(uint32_t *s_cnt, int lane, bool counted, uint32_t key, uint32_t F) {
+  uint32_t present = wave_or(counted ? (1u << key) : 0u);
+  while (present) {
+    const uint32_t k = __builtin_ctz(present);
+    present &= present - 1;
+    const bool in = counted && key == k;
+    uint32_t mycnt = 0;
+#pragma unroll
+    for (int ff = 0; ff < 19; ff++) {
+      const unsigned long long m = __ballot(in && ((F >> ff) & 1u));
+      mycnt = (lane == ff) ? (uint32_t)__popcll(m) : mycnt;
+    }
+    if (lane < 19 && mycnt) atomicAdd(&s_cnt[k * 19 + lane], mycnt);
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kCheckThreads) void k_check(StreamView sv, int64_t x0, int64_t x1, int R, CountsDev cd,
+                                                         unsigned long long *__restrict__ bitmap,
+                                                         uint32_t *__restrict__ words) {
+  constexpr bool EAGER = MODE == MODE_EAGER;
+  constexpr bool COUNTS = MODE == MODE_COUNTS || MODE == MODE_BYKEY;
+  constexpr bool BYKEY = MODE == MODE_BYKEY;
+  __shared__ __attribute__((aligned(16))) uint8_t s_win[kWin + 64];
+  __shared__ uint32_t s_inv[kInvWords];
+  __shared__ int32_t s_lens[kLdsLens];
+  __shared__ unsigned long long s_acc[19 + 21 + 3];  // totals, positions per key, succ/tff/halo
+  __shared__ uint32_t s_cnt[BYKEY ? 21 * 19 : 1];
+  const int lane = lane_id();
+  const int32_t *lensL = nullptr;
+  if (sv.nref <= kLdsLens) {
+    for (int i = threadIdx.x; i < sv.nref; i += kCheckThreads) s_lens[i] = (int32_t)sv.lens[i];
+    lensL = s_lens;
+  }
+  for (int i = threadIdx.x; i < 19 + 21 + 3; i += kCheckThreads) s_acc[i] = 0;
+  if (BYKEY)
+    for (int i = threadIdx.x; i < 21 * 19; i += kCheckThreads) s_cnt[i] = 0;
+
+  const int64_t x0a = x0 & ~(int64_t)63;
+  const int64_t ntiles = (x1 - x0a + kTile - 1) / kTile;
+  Acc acc;
+  acc.clear();
+  int since_flush = 0;
+
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t base = x0a + t * kTile;
+    __syncthreads();
+    {  // stage the window and build the op-validity bitmap (16 bytes per lane per step)
+      const uint4 *src = reinterpret_cast<const uint4 *>(sv.u + base);
+      uint4 *dst = reinterpret_cast<uint4 *>(s_win);
+      uint16_t *inv16 = reinterpret_cast<uint16_t *>(s_inv);
+      for (int i = threadIdx.x; i < kWin / 16; i += kCheckThreads) {
+        const uint4 v = src[i];
+        dst[i] = v;
+        inv16[i] = (uint16_t)(inv_nibble(v.x) | (inv_nibble(v.y) << 4) | (inv_nibble(v.z) << 8) | (inv_nibble(v.w) << 12));
+      }
+      if (threadIdx.x < 4) s_inv[kWin / 32 + threadIdx.x] = 0;
+    }
+    __syncthreads();
+    const Tile tl{s_win, s_inv, base};
+    const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
+#pragma unroll 1
+    for (int j = 0; j < kTile / (4 * kCheckThreads); j++) {
+      const int g = j * kCheckThreads + threadIdx.x;  // group of 4 consecutive positions
+      const int64_t xg = base + 4 * g;
+      uint32_t W[10];
+#pragma unroll
+      for (int q = 0; q < 10; q++) W[q] = w32[g + q];
+      uint32_t wd[4];
+#pragma unroll
+      for (int o = 0; o < 4; o++) {
+        const int64_t x = xg + o;
+        int32_t f[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) f[q] = (int32_t)__builtin_amdgcn_alignbyte(W[q + 1], W[q], o);
+        uint32_t w = (x >= x0 && x < x1) ? check_first<EAGER>(tl, sv, lensL, x, R, f) : W_NONE;
+        wd[o] = w;
+      }
+      if (MODE == MODE_WORDS) {
+#pragma unroll
+        for (int o = 0; o < 4; o++)
+          if (wd[o] != W_NONE && wd[o] != W_PASS0) words[xg + o - x0] = wd[o];
+      }
+      // first-record-pass bits: nibble per lane → 16 lanes per 64-bit word; k_chains turns them into calls
+      uint32_t nib = 0;
+#pragma unroll
+      for (int o = 0; o < 4; o++) nib |= (wd[o] == W_PASS0) ? (1u << o) : 0u;
+      uint64_t v = (uint64_t)nib << (4 * (lane & 15));
+      v |= shfl_xor64(v, 1);
+      v |= shfl_xor64(v, 2);
+      v |= shfl_xor64(v, 4);
+      v |= shfl_xor64(v, 8);
+      if ((lane & 15) == 0 && xg < x1) bitmap[(xg - x0a) >> 6] = v;  // word holds >= 1 position < x1
+      if (!COUNTS) continue;
+#if SBAM_ABLATE == 3  // timing experiment only: no counting
+      continue;
+#endif
+      uint32_t Fo[4];
+#pragma unroll
+      for (int o = 0; o < 4; o++) {
+        uint32_t key = 0;
+        bool counted = false;
+        Fo[o] = 0;
+        if (wd[o] != W_NONE && wd[o] != W_PASS0) Fo[o] = acc.classify<BYKEY>(wd[o], cd, key, counted);
+        if (BYKEY) bykey_count(s_cnt, lane, counted, key, Fo[o]);
+      }
+      const uint32_t x1a = Fo[0] ^ Fo[1], c1 = Fo[0] & Fo[1];
+      const uint32_t x2a = Fo[2] ^ Fo[3], c2 = Fo[2] & Fo[3];
+      const uint32_t ones = x1a ^ x2a, c3 = x1a & x2a;
+      acc.pl.add(ones, c1 ^ c2 ^ c3, (c1 & c2) | (c3 & (c1 ^ c2)));
+    }
+    if (COUNTS) {
+      if (++since_flush == kFlushTiles) {
+        flush_acc(acc, s_acc, lane);
+        since_flush = 0;
+      }
+    }
+  }
+  if (COUNTS) {
+    flush_acc(acc, s_acc, lane);
+    __syncthreads();
+    if (threadIdx.x < 19 && s_acc[threadIdx.x]) atomicAdd(&cd.totals[threadIdx.x], s_acc[threadIdx.x]);
+    if (threadIdx.x >= 32 && threadIdx.x < 53) {
+      const int k = threadIdx.x - 32;
+      if (s_acc[19 + k]) atomicAdd(&cd.positions[k], s_acc[19 + k]);
+    }
+    if (threadIdx.x >= 64 && threadIdx.x < 67 && s_acc[40 + threadIdx.x - 64])
+      atomicAdd(&cd.scalars[1 + threadIdx.x - 64], s_acc[40 + threadIdx.x - 64]);
+    if (BYKEY)
+      for (int i = threadIdx.x; i < 21 * 19; i += kCheckThreads)
+        if (s_cnt[i]) atomicAdd(&cd.counts[i], (unsigned long long)s_cnt[i]);
+  }
+}
+
+// ---- FindRecordStart ---------------------------------------------------------------------------------------
+// One workgroup per start offset scans 256 positions per step with the eager checker (global reads) until the
+// first true call; with a success bitmap covering [bx0, bx1) the covered prefix is read from the bitmap.
+// out = found offset, -1 = None, -2 = HALO.
+__global__ __launch_bounds__(kCheckThreads) void k_find_record_starts(StreamView sv, const int64_t *__restrict__ xs,
+                                                                      int R, int64_t max_read_size,
+                                                                      const unsigned long long *__restrict__ bitmap,
+                                                                      int64_t bx0, int64_t bx1,
+                                                                      int64_t *__restrict__ out) {
+  __shared__ unsigned long long s_best;
+  __shared__ int s_halo;
+  const int64_t x0 = xs[blockIdx.x];
+  if (threadIdx.x == 0) { s_best = ~0ull; s_halo = 0; }
+  __syncthreads();
+  if (x0 < 0) {
+    if (threadIdx.x == 0) out[blockIdx.x] = -1;
+    return;
+  }
+  const int64_t lim = min(sv.L, x0 + max_read_size);
+  int64_t x = x0;
+  if (bitmap && x0 >= bx0 && x0 < bx1) {
+    const int64_t blim = min(lim, bx1);
+    for (int64_t wb = (x0 - bx0) >> 6; bx0 + (wb << 6) < blim; wb += kCheckThreads) {
+      const int64_t wi = wb + threadIdx.x;
+      const int64_t wx = bx0 + (wi << 6);
+      if (wx < blim) {
+        unsigned long long m = bitmap[wi];
+        if (wx < x0) m &= ~0ull << (x0 - wx);
+        if (m) {
+          const int64_t hit = wx + __ffsll((long long)m) - 1;
+          if (hit < blim) atomicMin(&s_best, (unsigned long long)hit);
+        }
+      }
+      __syncthreads();
+      if (s_best != ~0ull) break;
+      __syncthreads();
+    }
+    x = blim;
+  }
+  while (s_best == ~0ull && x < lim && !s_halo) {
+    const int64_t p = x + threadIdx.x;
+    if (p < lim) {
+      const uint32_t word = check_chain<true>(sv, GlobalBytes{sv.u}, p, p, 0, R);
+      if (word == W_HALO) s_halo = 1;
+      else if (word & W_SUCC) atomicMin(&s_best, (unsigned long long)p);
+    }
+    __syncthreads();
+    x += kCheckThreads;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = (s_best != ~0ull) ? (int64_t)s_best : (s_halo ? -2 : -1);
+}
+
+// ---- record chain ------------------------------------------------------------------------------------------
+// counts[i] = records r with r < x_end from xs[i]; -2 when the chain left a shard's bytes (HALO), -3 truncated.
+__global__ void k_record_counts(StreamView sv, const int64_t *__restrict__ xs, const int64_t *__restrict__ xe, int64_t n,
+                                int64_t *__restrict__ counts) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int64_t x = xs[i];
+  const int64_t end = xe[i];
+  int64_t c = 0;
+  if (x >= 0) {
+    while (x < end) {
+      if (x + 4 > sv.L) { c = sv.eof_real ? -3 : -2; break; }
+      const int32_t bs = g_i32(sv.u, x);
+      if (bs < 0 || x + 4 + (int64_t)bs > sv.L) { c = sv.eof_real ? -3 : -2; break; }
+      c++;
+      x += 4 + (int64_t)bs;
+    }
+  }
+  counts[i] = c;
+}
+
+__global__ void k_record_offsets(StreamView sv, int64_t x, int64_t end, int64_t *__restrict__ offs, int64_t cap,
+                                 int64_t *__restrict__ n_out) {
+  int64_t c = 0;
+  while (x < end) {
+    if (x + 4 > sv.L) { c = -3 - c; break; }
+    const int32_t bs = g_i32(sv.u, x);
+    if (bs < 0 || x + 4 + (int64_t)bs > sv.L) { c = -3 - c; break; }
+    if (c < cap) offs[c] = x;
+    c++;
+    x += 4 + (int64_t)bs;
+  }
+  *n_out = c;
+}
+
+// ---- launch wrappers ---------------------------------------------------------------------------------------
+static int check_grid(int64_t ntiles) { return (int)(ntiles < 1 ? 1 : ntiles > 2048 ? 2048 : ntiles); }
+static int64_t ntiles_of(int64_t x0, int64_t x1) { return (x1 - (x0 & ~(int64_t)63) + kTile - 1) / kTile; }
+static int chain_grid(int64_t x0, int64_t x1) {
+  const int64_t words = (x1 - (x0 & ~(int64_t)63) + 63) >> 6;
+  const int64_t g = (words + 255) / 256;
+  return (int)(g < 1 ? 1 : g > 8192 ? 8192 : g);
+}
+
+hipError_t launch_check_full_counts(StreamView sv, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,
+                                    unsigned long long *bitmap, hipStream_t s) {
+  if (x1 <= x0) return hipSuccess;
+  const int g = check_grid(ntiles_of(x0, x1));
+  if (by_key)
+    hipLaunchKernelGGL(k_check<MODE_BYKEY>, dim3(g), dim3(kCheckThreads), 0, s, sv, x0, x1, R, cd, bitmap, nullptr);
+  else
+    hipLaunchKernelGGL(k_check<MODE_COUNTS>, dim3(g), dim3(kCheckThreads), 0, s, sv, x0, x1, R, cd, bitmap, nullptr);
+  hipLaunchKernelGGL(k_chains, dim3(chain_grid(x0, x1)), dim3(256), 0, s, sv, x0, x1, R, bitmap, cd, by_key, nullptr);
+  return hipGetLastError();
+}
+hipError_t launch_check_eager(StreamView sv, int64_t x0, int64_t x1, int32_t R, unsigned long long *bitmap,
+                              hipStream_t s) {
+  if (x1 <= x0) return hipSuccess;
+  hipLaunchKernelGGL(k_check<MODE_EAGER>, dim3(check_grid(ntiles_of(x0, x1))), dim3(kCheckThreads), 0, s, sv, x0, x1,
+                     R, CountsDev{}, bitmap, nullptr);
+  hipLaunchKernelGGL(k_chains, dim3(chain_grid(x0, x1)), dim3(256), 0, s, sv, x0, x1, R, bitmap, CountsDev{}, 0, nullptr);
+  return hipGetLastError();
+}
+hipError_t launch_check_words(StreamView sv, int64_t x0, int64_t x1, int32_t R, uint32_t *words,
+                              unsigned long long *bitmap, hipStream_t s) {
+  if (x1 <= x0) return hipSuccess;
+  hipLaunchKernelGGL(k_check<MODE_WORDS>, dim3(check_grid(ntiles_of(x0, x1))), dim3(kCheckThreads), 0, s, sv, x0, x1,
+                     R, CountsDev{}, bitmap, words);
+  hipLaunchKernelGGL(k_chains, dim3(chain_grid(x0, x1)), dim3(256), 0, s, sv, x0, x1, R, bitmap, CountsDev{}, 0, words);
+  return hipGetLastError();
+}
+hipError_t launch_find_record_starts(StreamView sv, const int64_t *x0, int64_t n, int32_t R, int64_t mrs,
+                                     const unsigned long long *bitmap, int64_t bx0, int64_t bx1, int64_t *out,
+                                     hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_find_record_starts, dim3((unsigned)n), dim3(kCheckThreads), 0, s, sv, x0, R, mrs, bitmap, bx0,
+                     bx1, out);
+  return hipGetLastError();
+}
+hipError_t launch_record_counts(StreamView sv, const int64_t *x0, const int64_t *xe, int64_t n, int64_t *counts,
+                                hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_record_counts, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, sv, x0, xe, n, counts);
+  return hipGetLastError();
+}
+hipError_t launch_record_offsets(StreamView sv, int64_t x0, int64_t xe, int64_t *offs, int64_t cap, int64_t *n_out,
+                                 hipStream_t s) {
+  hipLaunchKernelGGL(k_record_offsets, dim3(1), dim3(1), 0, s, sv, x0, xe, offs, cap, n_out);
+  return hipGetLastError();
+}
+
+}  // namespace sbam

@@ -41,6 +41,7 @@ struct CountsDev {  // mirrors sbam_counts (int64 fields) in device memory
   unsigned long long *rbe;  // [21][128]
   unsigned long long *pair;  // [19][19]
   unsigned long long *scalars;  // n_positions, n_success, n_too_few_fixed, n_halo
+  unsigned long long *totals;   // [19] per-flag totals over every counted position
 };
 
 constexpr int kScanChunk = 1 << 20;  // bytes per workgroup in the BGZF candidate scan
@@ -64,11 +65,13 @@ hipError_t launch_inflate(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *o
                           int32_t *status, int32_t *found, unsigned int *next_block, unsigned long long *first_err,
                           hipStream_t s);
 hipError_t launch_lower_bound(const Candidate *c, int64_t n, int64_t q, int64_t *out, hipStream_t s);
-hipError_t launch_check_full_counts(StreamView sv, int64_t x0, int64_t x1, int32_t R, CountsDev cd,
+// Bitmaps cover [x0 & ~63, x1): bit (x - (x0 & ~63)) = call at x (0 for x < x0).
+hipError_t launch_check_full_counts(StreamView sv, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,
                                     unsigned long long *bitmap, hipStream_t s);
 hipError_t launch_check_eager(StreamView sv, int64_t x0, int64_t x1, int32_t R, unsigned long long *bitmap,
                               hipStream_t s);
-hipError_t launch_check_words(StreamView sv, int64_t x0, int64_t x1, int32_t R, uint32_t *words, hipStream_t s);
+hipError_t launch_check_words(StreamView sv, int64_t x0, int64_t x1, int32_t R, uint32_t *words,
+                              unsigned long long *bitmap, hipStream_t s);
 hipError_t launch_find_record_starts(StreamView sv, const int64_t *x0, int64_t n, int32_t R, int64_t max_read_size,
                                      const unsigned long long *bitmap, int64_t bitmap_x0, int64_t bitmap_x1,
                                      int64_t *out, hipStream_t s);

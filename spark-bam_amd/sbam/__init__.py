@@ -87,7 +87,7 @@ class _Error(ctypes.Structure):
 
 
 class _Counts(ctypes.Structure):
-    _fields_ = [("counts", ctypes.c_int64 * (21 * 19)), ("positions", ctypes.c_int64 * 21),
+    _fields_ = [("totals", ctypes.c_int64 * 19), ("counts", ctypes.c_int64 * (21 * 19)), ("positions", ctypes.c_int64 * 21),
                 ("reads_before_error", ctypes.c_int64 * (21 * 128)), ("pair_hist", ctypes.c_int64 * (19 * 19)),
                 ("n_positions", ctypes.c_int64), ("n_success", ctypes.c_int64),
                 ("n_too_few_fixed", ctypes.c_int64), ("n_halo", ctypes.c_int64)]
@@ -136,7 +136,7 @@ def load_library(path: str = LIB_PATH):
         "sbam_set_contig_lengths": (ctypes.c_int, [vp, i32, vp]),
         "sbam_check_eager": (ctypes.c_int, [vp, i64, i64, i32, vp]),
         "sbam_check_full_words": (ctypes.c_int, [vp, i64, i64, i32, vp]),
-        "sbam_check_full_counts": (ctypes.c_int, [vp, i64, i64, i32, P(_Counts), vp]),
+        "sbam_check_full_counts": (ctypes.c_int, [vp, i64, i64, i32, i32, P(_Counts), vp]),
         "sbam_find_record_start": (ctypes.c_int, [vp, i64, i32, i32, P(i32), P(_Pos), P(i32)]),
         "sbam_file_splits": (ctypes.c_int, [i64, i64, vp, vp, i64, P(i64)]),
         "sbam_split_records": (ctypes.c_int, [vp, P(_SplitArgs), i64, i64, vp, vp, vp]),
@@ -197,17 +197,14 @@ def _pos(p: _Pos) -> Pos:
 @dataclass
 class Counts:
     """full-check reductions (check/.../full/error/Counts.scala; FullCheck.scala:141-191)."""
-    by_key: np.ndarray  # [21, 19]
+    totals: np.ndarray  # [19] per flag over every counted position ("Total error counts")
+    by_key: np.ndarray  # [21, 19]: keys 1-2 always; every key when computed with by_key=True
     positions: np.ndarray  # [21]
     reads_before_error: np.ndarray  # [21, 128]
     pair_hist: np.ndarray  # [19, 19]
     n_positions: int
     n_success: int
     n_too_few_fixed: int
-
-    @property
-    def totals(self) -> np.ndarray:
-        return self.by_key.sum(axis=0)
 
     def total_error_counts(self) -> dict:
         t = self.totals
@@ -374,12 +371,14 @@ class BamFile:
         return out[: x1 - x0]
 
     def check_full_counts(self, x0: int = 0, x1: Optional[int] = None, reads_to_check: int = READS_TO_CHECK,
-                          want_bitmap: bool = False):
+                          want_bitmap: bool = False, by_key: bool = False):
         x1 = self.uncompressed_size if x1 is None else x1
         c = _Counts()
         bm = np.zeros((x1 - x0 + 63) // 64 + 1, np.uint64) if want_bitmap else None
-        self._check(self.L.sbam_check_full_counts(self.ctx, x0, x1, reads_to_check, ctypes.byref(c), _ptr(bm)))
-        counts = Counts(np.ctypeslib.as_array(c.counts).reshape(21, 19).copy(),
+        self._check(self.L.sbam_check_full_counts(self.ctx, x0, x1, reads_to_check, 1 if by_key else 0,
+                                                  ctypes.byref(c), _ptr(bm)))
+        counts = Counts(np.ctypeslib.as_array(c.totals).copy(),
+                        np.ctypeslib.as_array(c.counts).reshape(21, 19).copy(),
                         np.ctypeslib.as_array(c.positions).copy(),
                         np.ctypeslib.as_array(c.reads_before_error).reshape(21, 128).copy(),
                         np.ctypeslib.as_array(c.pair_hist).reshape(19, 19).copy(),

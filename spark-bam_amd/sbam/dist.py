@@ -21,7 +21,7 @@ from typing import Callable, List, Optional, Sequence
 
 import numpy as np
 
-N_COUNT_WORDS = 21 * 19 + 21 + 21 * 128 + 19 * 19 + 3
+N_COUNT_WORDS = 19 + 21 * 19 + 21 + 21 * 128 + 19 * 19 + 3
 
 
 def hadoop_splits(file_size: int, split_size: int):
@@ -72,14 +72,14 @@ class ShardResult:
 
 
 def pack_counts(c) -> np.ndarray:
-    return np.concatenate([c.by_key.ravel(), c.positions, c.reads_before_error.ravel(), c.pair_hist.ravel(),
+    return np.concatenate([c.totals, c.by_key.ravel(), c.positions, c.reads_before_error.ravel(), c.pair_hist.ravel(),
                            np.array([c.n_success, c.n_too_few_fixed, c.n_positions], np.int64)]).astype(np.int64)
 
 
 def unpack_counts(v: np.ndarray) -> dict:
     o = 0
     out = {}
-    for name, n, shape in (("by_key", 21 * 19, (21, 19)), ("positions", 21, (21,)),
+    for name, n, shape in (("totals", 19, (19,)), ("by_key", 21 * 19, (21, 19)), ("positions", 21, (21,)),
                            ("reads_before_error", 21 * 128, (21, 128)), ("pair_hist", 19 * 19, (19, 19))):
         out[name] = v[o:o + n].reshape(shape)
         o += n

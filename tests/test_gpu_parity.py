@@ -57,16 +57,38 @@ def test_eager_matches_records(name, gpu_files):
 
 @pytest.mark.parametrize("name", ALL_BAMS)
 @pytest.mark.parametrize("reads_to_check", [10, 1, 3])
-def test_full_counts(name, reads_to_check, gpu_files, oracle_files):
+@pytest.mark.parametrize("by_key", [False, True])
+def test_full_counts(name, reads_to_check, by_key, gpu_files, oracle_files):
     g, o = gpu_files(name), oracle_files(name)
     counts, npos, rbe, nsucc = o.counts_range(0, o.L, reads_to_check)
-    c, bits = g.check_full_counts(0, o.L, reads_to_check, want_bitmap=True)
-    assert np.array_equal(c.by_key, counts)
+    c, bits = g.check_full_counts(0, o.L, reads_to_check, want_bitmap=True, by_key=by_key)
+    assert np.array_equal(c.totals, counts.sum(0))
+    if by_key:
+        assert np.array_equal(c.by_key, counts)
+    else:
+        assert np.array_equal(c.by_key[:3], counts[:3])
     assert np.array_equal(c.positions, npos)
     assert np.array_equal(c.reads_before_error, rbe)
     assert c.n_success == nsucc
     w = o.check_full_range(0, o.L, reads_to_check)
     assert np.array_equal(bits, (w & 0x80000000) != 0)
+
+
+@pytest.mark.parametrize("name", ["2.bam", "5k.bam"])
+def test_check_unaligned_ranges(name, gpu_files, oracle_files):
+    """Sub-ranges with arbitrary (non 64-aligned) ends: words, counts, eager bitmap."""
+    g, o = gpu_files(name), oracle_files(name)
+    rng = np.random.default_rng(11)
+    for _ in range(6):
+        x0 = int(rng.integers(0, o.L - 1))
+        x1 = int(min(o.L, x0 + rng.integers(1, 200000)))
+        want = o.check_full_range(x0, x1)
+        assert np.array_equal(g.check_full_words(x0, x1), want)
+        c, bits = g.check_full_counts(x0, x1, want_bitmap=True)
+        cnt, npos, _, ns = o.counts_range(x0, x1)
+        assert np.array_equal(c.totals, cnt.sum(0)) and np.array_equal(c.positions, npos) and c.n_success == ns
+        assert np.array_equal(bits, (want & 0x80000000) != 0)
+        assert np.array_equal(g.check_eager(x0, x1), (want & 0x80000000) != 0)
 
 
 def test_find_block_start_golden(gpu_files):
