@@ -355,6 +355,34 @@ SB_DEV int slow_decode(uint64_t bb, int root, const uint16_t *cnt, const uint16_
 }
 
 enum : int { S_NEXT = 0, S_HDR = 1, S_HUFF = 2, S_COPY = 3, S_STORED = 4, S_DONE = 5, S_EXIT = 6 };
+
+// Per-lane output ring in LDS: the last 64 output bytes of the lane's block (stride 68 B so the 64 lanes of a
+// wave hit distinct banks).  Bytes are emitted into the ring and leave it as aligned 16-B global stores (or byte
+// stores for a block's partial first/last chunk, which share a 16-B chunk with the neighbouring block).
+// Copies with distance <= 56 read their source from the ring, longer ones from global memory (aligned 8-B pairs).
+constexpr int kRingStride = 68;
+constexpr int kRingNear = 56;
+
+SB_DEV void ring_flush(uint8_t *&fp, const uint8_t *o, const uint8_t *ring, bool final) {
+  for (;;) {
+    const uintptr_t f = reinterpret_cast<uintptr_t>(fp), oo = reinterpret_cast<uintptr_t>(o);
+    const uintptr_t cend = (f & ~(uintptr_t)15) + 16;
+    if ((f & 15) == 0 && f + 16 <= oo) {
+      const uint32_t *r = reinterpret_cast<const uint32_t *>(ring + (f & 63));
+      *reinterpret_cast<uint4 *>(fp) = make_uint4(r[0], r[1], r[2], r[3]);
+      fp += 16;
+    } else if ((f & 15) != 0 && cend <= oo) {
+      for (uintptr_t q = f; q < cend; q++) *reinterpret_cast<uint8_t *>(q) = ring[q & 63];
+      fp = reinterpret_cast<uint8_t *>(cend);
+    } else {
+      if (final)
+        for (uintptr_t q = f; q < oo; q++) *reinterpret_cast<uint8_t *>(q) = ring[q & 63];
+      if (final) fp = const_cast<uint8_t *>(o);
+      return;
+    }
+  }
+}
+
 enum : int32_t { INF_OK = 0, INF_SHORT = 1, INF_DATA = 2 };
 
 __global__ __launch_bounds__(256) void k_inflate(const uint8_t *__restrict__ d, int64_t D, BlockTable bt, uint8_t *out,
@@ -362,6 +390,8 @@ __global__ __launch_bounds__(256) void k_inflate(const uint8_t *__restrict__ d, 
                                                  int32_t *__restrict__ found, unsigned int *__restrict__ next_block,
                                                  unsigned long long *__restrict__ first_err) {
   __shared__ uint32_t s_len[32], s_dist[32];
+  __shared__ __attribute__((aligned(16))) uint8_t s_ring[256 * kRingStride];
+  uint8_t *ring = s_ring + threadIdx.x * kRingStride;
   if (threadIdx.x < 29) s_len[threadIdx.x] = kLenBase[threadIdx.x] | ((uint32_t)kLenExtra[threadIdx.x] << 16);
   if (threadIdx.x < 30) s_dist[threadIdx.x] = kDistBase[threadIdx.x] | ((uint32_t)kDistExtra[threadIdx.x] << 16);
   __syncthreads();
@@ -378,8 +408,9 @@ __global__ __launch_bounds__(256) void k_inflate(const uint8_t *__restrict__ d, 
   const uint32_t *inlim = nullptr;  // first dword the bit reader may not load (payload + footer)
   uint64_t bb = 0;
   int bc = 0;
-  uint8_t *o = nullptr, *ob = nullptr, *oe = nullptr;
+  uint8_t *o = nullptr, *ob = nullptr, *oe = nullptr, *fp = nullptr;
   int fin = 0, clen = 0, cdist = 0, sleft = 0;
+#define RING_PUT(b) (ring[reinterpret_cast<uintptr_t>(o) & 63] = (uint8_t)(b), o++)
 
   for (;;) {
     if (state == S_NEXT) {
@@ -396,6 +427,7 @@ __global__ __launch_bounds__(256) void k_inflate(const uint8_t *__restrict__ d, 
         bc = 32 - skip;
         ob = out + bt.uoff[blk];
         o = ob;
+        fp = ob;
         const int32_t us = bt.usize[blk];
         oe = ob + us;
         fin = 0;
@@ -500,7 +532,7 @@ __global__ __launch_bounds__(256) void k_inflate(const uint8_t *__restrict__ d, 
         bb >>= l;
         bc -= (int)l;
         if (sym < 256) {
-          *o++ = (uint8_t)sym;
+          RING_PUT(sym);
           if (o == oe) state = S_DONE;
         } else if (sym == 256) {
           if (fin) { err = (o == oe) ? INF_OK : INF_SHORT; state = S_DONE; }
@@ -539,25 +571,33 @@ __global__ __launch_bounds__(256) void k_inflate(const uint8_t *__restrict__ d, 
     if (state == S_COPY) {  // up to 8 bytes per step; an overlapping copy replicates its period
       const int room = (int)(oe - o);
       const int n = min(min(clen, 8), room);
-      const uint8_t *src = o - cdist;
+      const uintptr_t src = reinterpret_cast<uintptr_t>(o) - (uintptr_t)cdist;
       const int np = min(cdist, 8);
       uint64_t pat = 0;
+      if (cdist <= kRingNear) {  // source still in the ring
 #pragma unroll
-      for (int i = 0; i < 8; i++) pat |= (i < np) ? ((uint64_t)src[i] << (8 * i)) : 0ull;
-      for (int p = cdist; p < 8; p <<= 1) pat |= pat << (8 * p);
+        for (int i = 0; i < 8; i++) pat |= (i < np) ? ((uint64_t)ring[(src + i) & 63] << (8 * i)) : 0ull;
+      } else {  // source already flushed: two aligned 8-byte loads
+        const uint64_t *a8 = reinterpret_cast<const uint64_t *>(src & ~(uintptr_t)7);
+        const uint64_t lo = a8[0], hi = a8[1];
+        const int sh = (int)(src & 7) * 8;
+        pat = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+      }
+      if (cdist < 8) {
+        pat &= (1ull << (8 * cdist)) - 1;
+        for (int p = cdist; p < 8; p <<= 1) pat |= pat << (8 * p);
+      }
 #pragma unroll
       for (int i = 0; i < 8; i++)
-        if (i < n) o[i] = (uint8_t)(pat >> (8 * i));
-      o += n;
+        if (i < n) RING_PUT(pat >> (8 * i));
       clen -= n;
       if (o == oe) state = S_DONE;
       else if (clen == 0) state = S_HUFF;
     } else if (state == S_STORED) {
       const int n = min(min(sleft, 4), (int)(oe - o));
-      for (int i = 0; i < n; i++) o[i] = (uint8_t)(bb >> (8 * i));
+      for (int i = 0; i < n; i++) RING_PUT(bb >> (8 * i));
       bb >>= 8 * n;
       bc -= 8 * n;
-      o += n;
       sleft -= n;
       if (o == oe) state = S_DONE;
       else if (sleft == 0) {
@@ -565,6 +605,7 @@ __global__ __launch_bounds__(256) void k_inflate(const uint8_t *__restrict__ d, 
         else state = S_HDR;
       }
     }
+    if (state != S_EXIT && state != S_NEXT) ring_flush(fp, o, ring, state == S_DONE);
     if (state == S_DONE) {
       if (err != INF_OK) atomicMin(first_err, (unsigned long long)blk);
       status[blk] = err;
@@ -572,6 +613,7 @@ __global__ __launch_bounds__(256) void k_inflate(const uint8_t *__restrict__ d, 
       state = S_NEXT;
     }
   }
+#undef RING_PUT
 }
 
 // ================================================================================================
