@@ -87,6 +87,27 @@ def unpack_counts(v: np.ndarray) -> dict:
     return out
 
 
+def shard_pass(f, p: ShardPlan, split_size: int, R: int = 10) -> ShardResult:
+    """One shard's hot path once its stream is inflated (``f``: sbam.BamFile over the shard's bytes, or any
+    object with the same methods): full check of the positions of the blocks the shard owns (from its first
+    block to the block where the next shard starts), then the owned Hadoop splits' first records and counts."""
+    st, _, _, uo = f.blocks()
+    if p.owned_hi >= p.file_size:
+        x1 = f.uncompressed_size
+    else:
+        nb = f.find_block_start(p.owned_hi)
+        b = int(np.searchsorted(st, nb))
+        x1 = int(uo[b]) if b < st.size else f.uncompressed_size
+    counts = f.check_full_counts(0, x1, R)
+    recs = f.split_records(split_size, first=p.split_first, count=p.split_count, reads_to_check=R,
+                           use_success_bitmap=True) if p.split_count else []
+    return ShardResult(pack_counts(counts),
+                       np.array([r[0].block_pos for r in recs], np.int64),
+                       np.array([r[0].offset for r in recs], np.int64),
+                       np.array([int(r[1]) for r in recs], np.int64),
+                       np.array([r[2] for r in recs], np.int64))
+
+
 class GpuShard:
     """Per-rank GPU work for one shard: scan → inflate → full check (owned positions) → split records."""
 
@@ -108,24 +129,9 @@ class GpuShard:
                                    file_size=self.plan.file_size, inflate=False)
 
     def _once(self) -> ShardResult:
-        p, f = self.plan, self.f
-        f.reset()
-        f.run(contig_lengths=self.contig_lengths)
-        st, _, _, uo = f.blocks()
-        if p.owned_hi >= p.file_size:
-            x1 = f.uncompressed_size
-        else:
-            nb = f.find_block_start(p.owned_hi)
-            b = int(np.searchsorted(st, nb))
-            x1 = int(uo[b]) if b < st.size else f.uncompressed_size
-        counts = f.check_full_counts(0, x1, self.R)
-        recs = f.split_records(self.split_size, first=p.split_first, count=p.split_count,
-                               reads_to_check=self.R, use_success_bitmap=True) if p.split_count else []
-        return ShardResult(pack_counts(counts),
-                           np.array([r[0].block_pos for r in recs], np.int64),
-                           np.array([r[0].offset for r in recs], np.int64),
-                           np.array([int(r[1]) for r in recs], np.int64),
-                           np.array([r[2] for r in recs], np.int64))
+        self.f.reset()
+        self.f.run(contig_lengths=self.contig_lengths)
+        return shard_pass(self.f, self.plan, self.split_size, self.R)
 
     def step(self) -> ShardResult:
         while True:
