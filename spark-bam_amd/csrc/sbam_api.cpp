@@ -54,9 +54,14 @@ struct sbam_ctx {
   int64_t bm_x0 = 0, bm_x1 = 0;
   bool bm_valid = false;
   int32_t bm_R = -1;
-  // inflate scratch
+  // inflate scratch: v2 per-lane Huffman tables; token pages of the decode → resolve path
   uint16_t *d_scratch = nullptr;
   int nlanes = 0;
+  uint8_t *d_pool = nullptr;
+  size_t pool_cap = 0;  // bytes
+  int32_t *d_blkpage = nullptr;
+  size_t blkpage_cap = 0;
+  unsigned int *d_icnt = nullptr;  // decode work, pool pages used, resolve work
   // small device scratch
   int64_t *d_small = nullptr;  // 64 int64
   unsigned long long *d_counts = nullptr;
@@ -232,6 +237,9 @@ void sbam_close(sbam_ctx *c) {
   dfree(c->d_lens);
   dfree(c->d_bitmap);
   dfree(c->d_scratch);
+  dfree(c->d_pool);
+  dfree(c->d_blkpage);
+  dfree(c->d_icnt);
   dfree(c->d_small);
   dfree(c->d_counts);
   for (auto &kv : c->ev) {
@@ -432,26 +440,57 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
   HIPCHK(c, ensure(&c->d_u, &c->u_cap, (size_t)L + kStreamPad));
   HIPCHK(c, hipMemsetAsync(c->d_u + L, 0, kStreamPad, c->stream));
   const int64_t nb = c->nblocks;
-  int64_t cap_lanes = 256LL * 512;  // ≤ 512 lanes (8 waves) per CU
-  if (const char *e = getenv("SBAM_INFLATE_LANES")) cap_lanes = std::max<int64_t>(256, atoll(e));
-  int lanes = (int)std::min<int64_t>(((nb + 255) / 256) * 256, (cap_lanes / 256) * 256);
-  if (lanes < 256) lanes = 256;
-  if (lanes > c->nlanes) {
-    dfree(c->d_scratch);
-    HIPCHK(c, dalloc(&c->d_scratch, (size_t)lanes * kInflateScratchU16));
-    c->nlanes = lanes;
-  }
   HIPCHK(c, ensure(&c->d_status, &c->status_cap, nb));
   HIPCHK(c, ensure(&c->d_found, &c->found_cap, nb));
   int32_t *d_status = c->d_status, *d_found = c->d_found;
   const unsigned long long none = ~0ull;
-  HIPCHK(c, hipMemcpyAsync(c->d_small + 2, &none, 8, hipMemcpyHostToDevice, c->stream));
   BlockTable bt{c->d_bstart, c->d_bh, c->d_bc, c->d_bu, c->d_buoff, nb};
-  {
+  if (getenv("SBAM_INFLATE_V2")) {  // previous single-kernel path (A/B only)
+    int64_t cap_lanes = 256LL * 512;
+    int lanes = (int)std::min<int64_t>(((nb + 255) / 256) * 256, (cap_lanes / 256) * 256);
+    if (lanes < 256) lanes = 256;
+    if (lanes > c->nlanes) {
+      dfree(c->d_scratch);
+      HIPCHK(c, dalloc(&c->d_scratch, (size_t)lanes * kInflateScratchU16));
+      c->nlanes = lanes;
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_small + 2, &none, 8, hipMemcpyHostToDevice, c->stream));
     Timer t(c, "inflate");
     HIPCHK(c, launch_inflate(c->d_comp, c->D, bt, c->d_u, c->d_scratch, lanes, d_status, d_found,
                              reinterpret_cast<unsigned int *>(c->d_small + 3),
                              reinterpret_cast<unsigned long long *>(c->d_small + 2), c->stream));
+  } else {
+    // token pool: ~0.7 B of tokens per output byte on BAM data; a full pool (flagged per block) doubles it
+    // and re-runs, up to the bound of 2 B per output byte (+ one partial page per block)
+    const size_t page_bytes = (size_t)kTokPage, per_page = page_bytes - 16;
+    size_t want = ((size_t)L / per_page + (size_t)nb + 1024) * page_bytes;
+    const size_t bound = (2 * (size_t)L / per_page + 2 * (size_t)nb + 1024) * page_bytes;
+    if (c->pool_cap > want) want = c->pool_cap;
+    HIPCHK(c, ensure(&c->d_blkpage, &c->blkpage_cap, nb));
+    if (!c->d_icnt) HIPCHK(c, dalloc(&c->d_icnt, 4));
+    const int dec_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256);
+    const int res_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256 * 8);
+    for (;;) {
+      if (c->pool_cap < want) {
+        dfree(c->d_pool);
+        c->pool_cap = 0;
+        HIPCHK(c, dalloc(&c->d_pool, want));
+        c->pool_cap = want;
+      }
+      const uint32_t npages = (uint32_t)std::min<size_t>(c->pool_cap / page_bytes, 0xffffffffu);
+      {
+        Timer t(c, "inflate");
+        HIPCHK(c, launch_inflate_tokens(c->d_comp, c->D, bt, c->d_u, c->d_pool, npages, c->d_blkpage, d_status,
+                                        d_found, c->d_icnt, dec_wgs, res_wgs, c->stream));
+      }
+      unsigned int used = 0;
+      HIPCHK(c, hipMemcpyAsync(&used, c->d_icnt + 1, 4, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      if (used <= npages || c->pool_cap >= bound) break;
+      want = std::min(bound, 2 * c->pool_cap);
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_small + 2, &none, 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_first_error(d_status, nb, reinterpret_cast<unsigned long long *>(c->d_small + 2), c->stream));
   }
   unsigned long long ferr = 0;
   HIPCHK(c, hipMemcpyAsync(&ferr, c->d_small + 2, 8, hipMemcpyDeviceToHost, c->stream));

@@ -1,0 +1,120 @@
+"""Inflate edge cases: BGZF files whose payloads cover every DEFLATE shape zlib emits (stored, fixed and
+dynamic Huffman blocks, Huffman-only, RLE, overlapping copies of every period up to 48, matches that reach
+back 32 KiB) plus corrupted and mis-sized payloads, checked against the oracle's zlib inflate
+(Inflater.inflate(buf, 0, ISIZE) semantics of bgzf/src/main/scala/org/hammerlab/bgzf/block/Stream.scala:31-71).
+
+The files are built here from Python's zlib (no reference fixtures cover these shapes; the reference's own
+BGZF goldens are exercised by test_gpu_parity)."""
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+EOF_BLOCK = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+
+
+def bgzf_block(payload: bytes, isize: int) -> bytes:
+    bsize = 18 + len(payload) + 8 - 1
+    hdr = b"\x1f\x8b\x08\x04\x00\x00\x00\x00\x00\xff\x06\x00BC\x02\x00" + struct.pack("<H", bsize)
+    return hdr + payload + struct.pack("<II", 0, isize & 0xffffffff)
+
+
+def deflate(data: bytes, level=6, strategy=zlib.Z_DEFAULT_STRATEGY, mem=8) -> bytes:
+    c = zlib.compressobj(level, zlib.DEFLATED, -15, mem, strategy)
+    return c.compress(data) + c.flush()
+
+
+def sample_inputs(seed: int):
+    r = np.random.default_rng(seed)
+    out = []
+    out.append(r.integers(0, 256, 60000, dtype=np.uint8).tobytes())                 # incompressible
+    out.append(b"A" * 60000)                                                          # dist-1 run, 258-B matches
+    for period in (2, 3, 5, 7, 13, 16, 17, 31, 40, 41, 47, 48, 64, 200):             # overlapping copies
+        unit = r.integers(0, 256, period, dtype=np.uint8).tobytes()
+        out.append((unit * (60000 // period + 1))[:60000])
+    text = b" ".join(b"SYN:1:FC:%d:%d:%d" % tuple(r.integers(0, 9999, 3)) for _ in range(4000))
+    out.append(text[:60000])
+    # BAM-like: qualities with runs, 2-bit bases, far repeats (up to 32 KiB back)
+    q = r.choice(np.frombuffer(b"#+5?EJ", np.uint8), 30000).tobytes()
+    far = r.integers(0, 256, 20000, dtype=np.uint8).tobytes()
+    out.append((q[:20000] + far + q[:5000] + far[:15000])[:60000])
+    out.append(b"x")
+    return out  # (an empty payload would end the stream: MetadataStream.scala:23-54)
+
+
+SHAPES = [(6, zlib.Z_DEFAULT_STRATEGY), (0, zlib.Z_DEFAULT_STRATEGY), (1, zlib.Z_DEFAULT_STRATEGY),
+          (9, zlib.Z_DEFAULT_STRATEGY), (6, zlib.Z_FILTERED), (6, zlib.Z_HUFFMAN_ONLY), (6, zlib.Z_RLE),
+          (6, zlib.Z_FIXED)]
+
+
+def build_file(seed: int, corrupt: int = 0, size_jitter: bool = False):
+    """A BGZF file of many blocks; `corrupt` flips that many random payload bits in ONE block."""
+    r = np.random.default_rng(seed + 1000)
+    blocks = []
+    for i, data in enumerate(sample_inputs(seed)):
+        level, strat = SHAPES[(i + seed) % len(SHAPES)]
+        p = bytearray(deflate(data, level, strat))
+        isize = len(data)
+        blocks.append([p, isize])
+    if corrupt:
+        b = int(r.integers(0, len(blocks)))
+        p = blocks[b][0]
+        if len(p):
+            for _ in range(corrupt):
+                k = int(r.integers(0, len(p) * 8))
+                p[k >> 3] ^= 1 << (k & 7)
+    if size_jitter:
+        b = int(r.integers(0, len(blocks)))
+        blocks[b][1] = max(0, blocks[b][1] + int(r.choice([-100, -1, 1, 7])))
+    return b"".join(bgzf_block(bytes(p), n) for p, n in blocks) + EOF_BLOCK
+
+
+def oracle_result(data: bytes):
+    import oracle
+    try:
+        f = oracle.BamFile(data)
+    except IOError as e:
+        return ("error", str(e))
+    return ("ok", f.u[: f.L].tobytes())
+
+
+def gpu_result(data: bytes):
+    import sbam
+    g = sbam.BamFile(data, inflate=False)
+    try:
+        n = g.inflate()
+    except sbam.InflateException as e:
+        g.close()
+        return ("error", str(e))
+    out = g.read_uncompressed(0, n)
+    g.close()
+    return ("ok", out)
+
+
+def test_oracle_roundtrips_every_shape():
+    data = build_file(0)
+    kind, out = oracle_result(data)
+    assert kind == "ok"
+    assert out == b"".join(sample_inputs(0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(4))
+def test_inflate_shapes_bit_exact(seed):
+    data = build_file(seed)
+    assert gpu_result(data) == oracle_result(data)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(24))
+def test_inflate_mis_sized_isize(seed):
+    data = build_file(seed, size_jitter=True)
+    assert gpu_result(data) == oracle_result(data)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(40))
+def test_inflate_corrupted_payloads(seed):
+    data = build_file(seed, corrupt=1 + seed % 4)
+    assert gpu_result(data) == oracle_result(data)
