@@ -480,8 +480,14 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
       const uint32_t npages = (uint32_t)std::min<size_t>(c->pool_cap / page_bytes, 0xffffffffu);
       {
         Timer t(c, "inflate");
-        HIPCHK(c, launch_inflate_tokens(c->d_comp, c->D, bt, c->d_u, c->d_pool, npages, c->d_blkpage, d_status,
-                                        d_found, c->d_icnt, dec_wgs, res_wgs, c->stream));
+        {
+          Timer t1(c, "inflate_decode");
+          HIPCHK(c, launch_inflate_decode(c->d_comp, c->D, bt, c->d_pool, npages, c->d_blkpage, d_status, d_found,
+                                          c->d_icnt, dec_wgs, c->stream));
+        }
+        Timer t2(c, "inflate_resolve");
+        HIPCHK(c, launch_inflate_resolve(bt, c->d_u, c->d_pool, c->d_blkpage, d_found, c->d_icnt, res_wgs,
+                                         c->stream));
       }
       unsigned int used = 0;
       HIPCHK(c, hipMemcpyAsync(&used, c->d_icnt + 1, 4, hipMemcpyDeviceToHost, c->stream));

@@ -18,6 +18,8 @@
 //     latency of back-reference loads.  Tokens become bytes in a 64-B per-lane LDS ring that leaves as
 //     aligned 16-B stores; copies with distance <= 40 read the ring, longer ones read HBM (4-B aligned
 //     loads + v_alignbyte).  Overlapping copies double their distance per step (the period stays valid).
+#include <type_traits>
+
 #include "sbam_internal.h"
 
 namespace sbam {
@@ -34,63 +36,62 @@ constexpr uint32_t kTokPad = 0xffffu;
 
 // ---- decode kernel: per-lane LDS slice ------------------------------------------------------------------------
 constexpr int kDecThreads = 256;
-constexpr int kSlice = 640;        // 256 × 640 B = 160 KiB
+constexpr int kSlice = 580;        // 145 dwords (odd): lanes at the same offset hit different banks
 constexpr int kLitSorted = 0;      // 288 B: lit/len symbols in canonical order (low 8 bits)
 constexpr int kClTab = 0;          //   during a dynamic header: 128-entry code-length-code table (u8: len<<5 | sym)
 constexpr int kLitHi = 288;        // 36 B: bit i set ⇔ canonical entry i is a symbol >= 256
-constexpr int kDistSorted = 324;   // 30 B: distance symbols in canonical order
-constexpr int kCnt = 416;          // 16 × u32: per-length counts, then fill cursors (builds only)
-constexpr int kLens = 480;         // 160 B: code lengths, one nibble per symbol (builds only)
-static_assert(kDecThreads * kSlice == 163840, "LDS budget");
+constexpr int kDistSorted = 324;   // 32 B: distance symbols in canonical order
+constexpr int kCnt = 356;          // 16 × u32: per-length counts, then fill cursors (builds only)
+constexpr int kLens = 420;         // 160 B: code lengths, one nibble per symbol (builds only)
+static_assert(kLens + 160 <= kSlice && kDecThreads * kSlice <= 163840, "LDS budget");
+// A lane that reaches a block header parks; parked lanes build their tables together once kParkMin of the
+// wave's 64 lanes wait (or none is left decoding).  A table build is a serial loop of a few thousand
+// instructions per lane, so builds started one lane at a time would cost the whole wave 64× that.
+#ifndef SBAM_PARK_MIN
+#define SBAM_PARK_MIN 16
+#endif
+constexpr int kParkMin = SBAM_PARK_MIN;
 
 constexpr uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-// Bit reader over one block payload.  bb holds bc valid bits (LSB first); nx is the next input dword, already
-// loaded (its load is issued one refill ahead, so the wave rarely waits on it); left = payload bits not yet
-// consumed (negative ⇒ the symbol needed bits past the payload: zlib returns for more input → SHORT).
-struct Bits {
-  uint64_t bb;
-  int bc;
-  int left;
-  uint32_t nx;
-  const uint32_t *inw;
-  SB_DEV void refill() {
-    if (bc <= 32) {
-      bb |= (uint64_t)nx << bc;
-      bc += 32;
-      nx = *inw++;
-    }
-  }
-  SB_DEV uint32_t peek(int n) const { return (uint32_t)bb & ((1u << n) - 1u); }
-  SB_DEV void drop(int n) {
-    bb >>= n;
-    bc -= n;
-    left -= n;
-  }
-};
+constexpr int kRing = 356;         // 128 B: per-lane input ring of 32 dwords (decode only; aliases kCnt/kLens)
+constexpr int kRingDw = 32;
+constexpr int kEpoch = 4;          // iterations between input-ring refills / token-chunk stores
+constexpr int kLoadDw = 16;        // dwords per ring refill (4 × 16-B loads)
+static_assert(kRing % 4 == 0 && kRing + 4 * kRingDw <= kSlice, "ring");
 
-// Canonical code of one alphabet: lim[l] = left-justified (15-bit) end of the length-l codes, bse[l] = index
-// of the first length-l symbol in canonical order minus its first code.  lim is non-decreasing in l.
+// Compile-time loop: f(integral_constant<I>) for I in [B, E) — the index is a constant in the IR from the
+// start, so the per-length arrays below stay in registers (SROA) instead of a scratch array.
+template <int B, int E, class F>
+SB_DEV void sfor(F &&f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    sfor<B + 1, E>(f);
+  }
+}
+
+// Canonical code of one alphabet: lim[l] = left-justified (15-bit) end of the length-l codes; pk[l] =
+// (bse[l] << 5) | l with bse[l] = index of the first length-l symbol in canonical order minus its first code.
+// lim is non-decreasing in l, so the code length of the next 15 bits `rev` is 1 + #{l < 15 : rev >= lim[l]}
+// and one select per length (v_cmp + v_cndmask) finds pk of that length.
 struct Canon {
   uint32_t lim[16];
-  int32_t bse[16];
+  int32_t pk[16];
 };
 
 // Decode the next symbol index: returns idx into the canonical symbol list (valid=false for an unassigned code,
 // which zlib reports after consuming 1 bit — the only incomplete codes it accepts are single 1-bit codes).
 SB_DEV int canon_decode(const Canon &c, uint64_t bb, int &len, bool &valid) {
   const uint32_t rev = __builtin_bitreverse32((uint32_t)bb) >> 17;
-  int L = 1;
-  int32_t B = c.bse[1];
-#pragma unroll
-  for (int l = 1; l < 15; l++) {  // mask arithmetic, not a select: keeps lim/bse in registers (no scratch)
-    const int32_t m = -(int32_t)(rev >= c.lim[l]);
-    L -= m;
-    B = (c.bse[l + 1] & m) | (B & ~m);
-  }
+  int32_t p = c.pk[1];
+  sfor<1, 15>([&](auto I) {
+    constexpr int l = decltype(I)::value;
+    p = rev >= c.lim[l] ? c.pk[l + 1] : p;
+  });
+  const int L = p & 31;
   valid = rev < c.lim[15];
   len = valid ? L : 1;
-  return valid ? (int)(rev >> (15 - L)) + B : 0;
+  return valid ? (int)(rev >> (15 - L)) + (p >> 5) : 0;
 }
 
 // Build the canonical structures of nsym code lengths (nibbles at LENS[sym0 ...]) into sorted (+hi bitmap).
@@ -101,77 +102,154 @@ SB_DEV int canon_build(uint8_t *sl, int sym0, int nsym, int sorted_off, bool lit
   const uint32_t *lens = reinterpret_cast<const uint32_t *>(sl + kLens);
 #pragma unroll
   for (int i = 0; i < 16; i++) cnt[i] = 0;
-  for (int s = 0; s < nsym; s++) {
+  // count pass, 8 nibbles per step (the unused tail of a dword is masked off)
+  for (int s = 0; s < nsym; s += 8) {
     const int n = sym0 + s;
-    const uint32_t v = (lens[n >> 3] >> (4 * (n & 7))) & 15u;
-    if (v) atomicAdd(&cnt[v], 1u);
-  }
-  uint32_t k[16];
+    const uint64_t two = (uint64_t)lens[n >> 3] | ((uint64_t)lens[(n >> 3) + 1] << 32);
+    uint32_t w = (uint32_t)(two >> (4 * (n & 7)));
+    if (nsym - s < 8) w &= (1u << (4 * (nsym - s))) - 1u;
 #pragma unroll
-  for (int i = 0; i < 16; i++) k[i] = cnt[i];
+    for (int j = 0; j < 8; j++) {
+      const uint32_t v = (w >> (4 * j)) & 15u;
+      if (v) atomicAdd(&cnt[v], 1u);
+    }
+  }
   int left = 1, maxl = 0;
+  bool over = false;
   uint32_t code = 0;
   int32_t offs = 0;
-#pragma unroll
-  for (int l = 1; l <= 15; l++) {
-    left = 2 * left - (int)k[l];
-    if (k[l]) maxl = l;
-    c.lim[l] = (code + k[l]) << (15 - l);
-    c.bse[l] = offs - (int32_t)code;
+  sfor<1, 16>([&](auto I) {
+    constexpr int l = decltype(I)::value;
+    const uint32_t k = cnt[l];
+    left = 2 * left - (int)k;
+    over |= left < 0;
+    maxl = k ? l : maxl;
+    c.lim[l] = (code + k) << (15 - l);
+    c.pk[l] = (int32_t)(((uint32_t)(offs - (int32_t)code) << 5) | (uint32_t)l);
     cnt[l] = (uint32_t)offs;  // fill cursor
-    offs += (int32_t)k[l];
-    code = (code + k[l]) << 1;
-    if (left < 0) return -1;
-  }
+    offs += (int32_t)k;
+    code = (code + k) << 1;
+  });
   c.lim[0] = 0;
-  c.bse[0] = 0;
-  if (left > 0 && maxl > 1) return -1;
+  c.pk[0] = 0;
+  if (over || (left > 0 && maxl > 1)) return -1;
   if (lit) {
     uint32_t *hi = reinterpret_cast<uint32_t *>(sl + kLitHi);
 #pragma unroll
     for (int i = 0; i < 9; i++) hi[i] = 0;
   }
-  for (int s = 0; s < nsym; s++) {
+  // fill pass: canonical order = by length, then by symbol (cursors advance in symbol order)
+  for (int s = 0; s < nsym; s += 8) {
     const int n = sym0 + s;
-    const uint32_t v = (lens[n >> 3] >> (4 * (n & 7))) & 15u;
-    if (v) {
-      const uint32_t pos = atomicAdd(&cnt[v], 1u);
-      sl[sorted_off + pos] = (uint8_t)s;
-      if (lit && s >= 256) atomicOr(reinterpret_cast<uint32_t *>(sl + kLitHi) + (pos >> 5), 1u << (pos & 31));
+    const uint64_t two = (uint64_t)lens[n >> 3] | ((uint64_t)lens[(n >> 3) + 1] << 32);
+    uint32_t w = (uint32_t)(two >> (4 * (n & 7)));
+    if (nsym - s < 8) w &= (1u << (4 * (nsym - s))) - 1u;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint32_t v = (w >> (4 * j)) & 15u;
+      if (v) {
+        const uint32_t pos = atomicAdd(&cnt[v], 1u);
+        sl[sorted_off + pos] = (uint8_t)(s + j);
+        if (lit && s + j >= 256)
+          atomicOr(reinterpret_cast<uint32_t *>(sl + kLitHi) + (pos >> 5), 1u << (pos & 31));
+      }
     }
   }
   return 0;
 }
 
-// Token output: an 8-slot shift register (tk.x low half = oldest) flushed as one 16-B store per chunk.
+// Token output: an 8-slot shift register (t0 low half = oldest); a full chunk moves to the pending chunk p,
+// which leaves as one 16-B store at the next epoch (so stores and input loads issue together, and no
+// load wait in between covers a fresh store).
 struct TokOut {
   uint32_t t0, t1, t2, t3;
+  uint32_t p0, p1, p2, p3;
   int n;
+  bool pend;
   uint64_t cur;  // byte offset of the next chunk in the pool
-  SB_DEV void put(uint32_t t) {
-    t0 = __builtin_amdgcn_alignbit(t1, t0, 16);
-    t1 = __builtin_amdgcn_alignbit(t2, t1, 16);
-    t2 = __builtin_amdgcn_alignbit(t3, t2, 16);
-    t3 = __builtin_amdgcn_alignbit(t, t3, 16);
-    n++;
-  }
 };
 
-// Store the full chunk; open a new page when this one is full.  Returns false on pool overflow.
-SB_DEV bool tok_flush(TokOut &to, uint8_t *pool, unsigned int *pool_next, uint32_t npages) {
-  *reinterpret_cast<uint4 *>(pool + to.cur) = make_uint4(to.t0, to.t1, to.t2, to.t3);
+// Store one chunk; open a new page when this one is full.  Returns false on pool overflow.
+SB_DEV bool tok_store(TokOut &to, uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint8_t *pool,
+                      unsigned int *pool_next, uint32_t npages) {
+  *reinterpret_cast<uint4 *>(pool + to.cur) = make_uint4(a, b, c, d);
   to.cur += 16;
-  to.n = 0;
   if ((to.cur & (kTokPage - 1)) == 0) {
-    const uint32_t p = atomicAdd(pool_next, 1u);
-    if (p >= npages) return false;
-    *reinterpret_cast<uint32_t *>(pool + to.cur - kTokPage) = p;  // link from the page just filled
-    to.cur = (uint64_t)p * kTokPage + 16;
+    const uint32_t pg = atomicAdd(pool_next, 1u);
+    if (pg >= npages) return false;
+    *reinterpret_cast<uint32_t *>(pool + to.cur - kTokPage) = pg;  // link from the page just filled
+    to.cur = (uint64_t)pg * kTokPage + 16;
   }
   return true;
 }
 
-enum : int { S_NEXT = 0, S_HDR = 1, S_HUFF = 2, S_STORED = 3, S_DONE = 4, S_EXIT = 5 };
+// Append one token; a completed chunk becomes pending (an older pending chunk is stored first: only at a
+// block's end or when more than 8 tokens arrive within one epoch).
+SB_DEV bool tok_put(TokOut &to, uint32_t t, uint8_t *pool, unsigned int *pool_next, uint32_t npages) {
+  to.t0 = __builtin_amdgcn_alignbit(to.t1, to.t0, 16);
+  to.t1 = __builtin_amdgcn_alignbit(to.t2, to.t1, 16);
+  to.t2 = __builtin_amdgcn_alignbit(to.t3, to.t2, 16);
+  to.t3 = __builtin_amdgcn_alignbit(t, to.t3, 16);
+  if (++to.n < 8) return true;
+  bool ok = true;
+  if (to.pend) ok = tok_store(to, to.p0, to.p1, to.p2, to.p3, pool, pool_next, npages);
+  to.p0 = to.t0;
+  to.p1 = to.t1;
+  to.p2 = to.t2;
+  to.p3 = to.t3;
+  to.pend = true;
+  to.n = 0;
+  return ok;
+}
+
+enum : int { S_NEXT = 0, S_HDR = 1, S_HUFF = 2, S_STORED = 3, S_DONE = 4, S_EXIT = 5, S_PARK = 6 };
+
+// Diagnostic build only (-DSBAM_DEC_STATS): per-wave cycle attribution of the decode loop, summed over waves.
+#ifdef SBAM_DEC_STATS
+__device__ unsigned long long g_dec_stats[16];
+#define DSTAT_MARK(slot)                                  \
+  do {                                                    \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();     \
+    ds_[slot] += t_ - dt_;                                \
+    dt_ = t_;                                             \
+  } while (0)
+#define DSTAT_ADD(slot, v) ds_[slot] += (v)
+#else
+#define DSTAT_MARK(slot) do {} while (0)
+#define DSTAT_ADD(slot, v) do {} while (0)
+#endif
+
+// Bit reader.  bb holds bc valid bits (LSB first); rp = block-relative index of the next payload dword to
+// enter bb; left = payload bits not yet consumed (negative ⇒ the symbol needed bits past the payload: zlib
+// returns for more input → SHORT).  While decoding symbols the dwords come from the lane's LDS ring
+// [rp, wp) (nx = ring[rp], read ahead); while parsing a block header they come straight from HBM.
+struct Bits {
+  uint64_t bb;
+  int bc;
+  int left;
+  uint32_t rp, wp, nx;
+  SB_DEV uint32_t peek(int n) const { return (uint32_t)bb & ((1u << n) - 1u); }
+  SB_DEV void drop(int n) {
+    bb >>= n;
+    bc -= n;
+    left -= n;
+  }
+  SB_DEV void refill_ring(const uint32_t *ring) {
+    if (bc <= 32) {
+      bb |= (uint64_t)nx << bc;
+      bc += 32;
+      rp++;
+      nx = ring[rp & (kRingDw - 1)];
+    }
+  }
+  SB_DEV void refill_hbm(const uint32_t *src) {
+    if (bc <= 32) {
+      bb |= (uint64_t)src[rp] << bc;
+      bc += 32;
+      rp++;
+    }
+  }
+};
 
 __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t *__restrict__ d, int64_t D,
                                                                    BlockTable bt, uint8_t *__restrict__ pool,
@@ -180,20 +258,31 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
                                                                    int32_t *__restrict__ status,
                                                                    int32_t *__restrict__ found,
                                                                    unsigned int *next_block) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_dec[kDecThreads * kSlice];
+  __shared__ __attribute__((aligned(16))) uint8_t s_dec[kDecThreads * kSlice + 16];  // +16: 2-dword lens reads
   uint8_t *sl = s_dec + threadIdx.x * kSlice;
   const uint8_t *litS = sl + kLitSorted;
   const uint32_t *litHi = reinterpret_cast<const uint32_t *>(sl + kLitHi);
   const uint8_t *distS = sl + kDistSorted;
+  uint32_t *ring = reinterpret_cast<uint32_t *>(sl + kRing);
+  const uint32_t *d32 = reinterpret_cast<const uint32_t *>(d);
 
   int state = S_NEXT;
   int64_t blk = -1;
-  Bits br{0, 0, 0, 0, nullptr};
-  TokOut to{0, 0, 0, 0, 0, 0};
+  const uint32_t *src = d32;  // the block's payload, from its first (4-B aligned) dword
+  uint32_t ldw = 0;           // payload dwords worth loading (payload + footer)
+  Bits br{0, 0, 0, 0, 0, 0};
+  uint32_t ld[kLoadDw];       // ring refill in flight (lands at the next epoch)
+  bool ldn = false;
+  TokOut to{0, 0, 0, 0, 0, 0, 0, 0, 0, false, 0};
   Canon lc, dc;
   int32_t o = 0, us = 0, err = INF_OK, sleft = 0, fin = 0;
+#ifdef SBAM_DEC_STATS
+  uint64_t ds_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t dt_ = __builtin_amdgcn_s_memtime();
+  const uint64_t dt0_ = dt_;
+#endif
 
-  for (;;) {
+  for (int it = 0;; it++) {
     if (state == S_NEXT) {
       blk = (int64_t)atomicAdd(next_block, 1u);
       if (blk >= bt.n) {
@@ -221,25 +310,71 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
             blk_page[blk] = (int32_t)p;
             to.cur = (uint64_t)p * kTokPage + 16;
             to.n = 0;
-            const uintptr_t a = reinterpret_cast<uintptr_t>(d + st + hs);
-            const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+            to.pend = false;
+            // word pointer derived from d by arithmetic only (an integer round trip would make it a flat
+            // pointer, whose loads the compiler must wait for together with every LDS access)
+            const int64_t a = st + hs;
+            src = d32 + (a >> 2);
+            ldw = (uint32_t)(((a & 3) + dlen + 8 + 3) >> 2);
             const int skip = (int)(a & 3) * 8;
-            br.bb = (uint64_t)w[0] >> skip;
+            br.bb = (uint64_t)src[0] >> skip;
             br.bc = 32 - skip;
-            br.nx = w[1];
-            br.inw = w + 2;
+            br.rp = 1;
             br.left = 8 * dlen;
-            br.refill();
-            state = S_HDR;
+            state = S_PARK;
           }
         }
       }
     }
     if (__all(state == S_EXIT)) break;
+    {  // release parked lanes together (see kParkMin)
+      const uint64_t pk = __ballot(state == S_PARK);
+      const uint64_t dc = __ballot(state == S_HUFF || state == S_STORED);
+      if (pk && (__popcll(pk) >= kParkMin || dc == 0) && state == S_PARK) state = S_HDR;
+      DSTAT_ADD(5, 1);
+      DSTAT_ADD(7, __popcll(dc));
+      DSTAT_ADD(8, __popcll(pk));
+    }
+    DSTAT_MARK(0);
+#ifdef SBAM_DEC_STATS
+    const bool any_hdr_ = __ballot(state == S_HDR) != 0;
+#endif
 
+    // --- epoch (wave-uniform): land the previous refill, store the pending token chunk, issue new refills.
+    // The loads issued here are first touched kEpoch iterations later, so the wait then is normally free.
+    if ((it & (kEpoch - 1)) == 0) {
+      const bool dec = state == S_HUFF || state == S_STORED;
+      if (ldn) {
+        if (dec) {
+#pragma unroll
+          for (int j = 0; j < kLoadDw; j++) ring[(br.wp + j) & (kRingDw - 1)] = ld[j];
+          br.wp += kLoadDw;
+          br.nx = ring[br.rp & (kRingDw - 1)];
+        }
+        ldn = false;  // a lane that left decoding drops its refill (its ring is rebuilt after the header)
+      }
+      if (to.pend && (dec || state == S_PARK || state == S_HDR)) {
+        if (!tok_store(to, to.p0, to.p1, to.p2, to.p3, pool, pool_next, npages)) {
+          err = INF_OVERFLOW;
+          state = S_DONE;
+        }
+        to.pend = false;
+      }
+      if (dec && br.wp - br.rp <= (uint32_t)(kRingDw - kLoadDw) && br.wp < ldw) {
+        const uint4 *g = reinterpret_cast<const uint4 *>(src + br.wp);
+        const uint4 x0 = g[0], x1 = g[1], x2 = g[2], x3 = g[3];
+        ld[0] = x0.x; ld[1] = x0.y; ld[2] = x0.z; ld[3] = x0.w;
+        ld[4] = x1.x; ld[5] = x1.y; ld[6] = x1.z; ld[7] = x1.w;
+        ld[8] = x2.x; ld[9] = x2.y; ld[10] = x2.z; ld[11] = x2.w;
+        ld[12] = x3.x; ld[13] = x3.y; ld[14] = x3.z; ld[15] = x3.w;
+        ldn = true;
+      }
+    }
+
+    DSTAT_MARK(1);
     if (state == S_HDR) {
       // --- block header (RFC 1951 §3.2.3); every read checks that the payload holds the bits (else SHORT)
-      br.refill();
+      br.refill_hbm(src);
       if (br.left < 3) {
         err = INF_SHORT;
         state = S_DONE;
@@ -249,7 +384,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
         br.drop(3);
         if (type == 0) {  // stored: skip to a byte boundary, LEN, NLEN
           br.drop(br.left & 7);
-          br.refill();
+          br.refill_hbm(src);
           if (br.left < 32) {
             err = INF_SHORT;
             state = S_DONE;
@@ -275,7 +410,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
           canon_build(sl, 288, 32, kDistSorted, false, dc);
           state = S_HUFF;
         } else if (type == 2) {  // dynamic codes
-          br.refill();
+          br.refill_hbm(src);
           if (br.left < 14) {
             err = INF_SHORT;
             state = S_DONE;
@@ -288,12 +423,12 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
             // code-length code lengths, 3 bits each in kClOrder order → packed 3-bit fields by symbol
             uint64_t clp = 0;
             if (ok == 1) {
-              br.refill();
+              br.refill_hbm(src);
               if (br.left < 3 * hclen) ok = -1;
               else {
 #pragma unroll
                 for (int i = 0; i < 19; i++) {
-                  if (i == 10) br.refill();
+                  if (i == 10) br.refill_hbm(src);
                   if (i < hclen) {
                     clp |= (uint64_t)br.peek(3) << (3 * kClOrder[i]);
                     br.drop(3);
@@ -320,7 +455,6 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
               }
               if (maxl == 0) {
                 // zlib decodes every code length as 0 (1 bit each), then fails on the missing EOB code
-                br.drop(0);
                 br.left -= hlit + hdist;
                 ok = br.left < 0 ? -1 : 0;
               } else if (left > 0) {
@@ -343,7 +477,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
                 int n = 0;
                 uint32_t prev = 0, acc = 0;
                 while (n < total) {
-                  br.refill();
+                  br.refill_hbm(src);
                   const uint32_t e = clt[br.peek(7)];
                   const int l = (int)(e >> 5);
                   const uint32_t sym = e & 31;
@@ -369,13 +503,17 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
                     v = 0;
                   }
                   if (n + rep > total) { ok = 0; break; }
-                  for (int r = 0; r < rep; r++) {
-                    acc |= v << (4 * (n & 7));
-                    if ((n & 7) == 7) {
-                      lens[n >> 3] = acc;
+                  const uint32_t pat = v * 0x11111111u;
+                  while (rep > 0) {  // up to the end of the current dword per step
+                    const int o8 = n & 7, k = min(rep, 8 - o8);
+                    const uint32_t m = (k == 8 ? 0xffffffffu : ((1u << (4 * k)) - 1u)) << (4 * o8);
+                    acc |= pat & m;
+                    n += k;
+                    rep -= k;
+                    if ((n & 7) == 0) {
+                      lens[(n >> 3) - 1] = acc;
                       acc = 0;
                     }
-                    n++;
                   }
                   prev = v;
                 }
@@ -393,14 +531,28 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
               state = S_DONE;
             }
           }
-        } else {
+        }
+        if (state == S_HDR) {  // type 3
           err = INF_DATA;  // invalid block type
           state = S_DONE;
         }
       }
+      if (state == S_HUFF || state == S_STORED) {
+        // the tables overwrote the ring: prime it from HBM (one wait per header round)
+        const uint4 *g = reinterpret_cast<const uint4 *>(src + br.rp);
+        const uint4 x0 = g[0], x1 = g[1], x2 = g[2], x3 = g[3];
+        const uint32_t q = br.rp;
+        ring[(q + 0) & 31] = x0.x; ring[(q + 1) & 31] = x0.y; ring[(q + 2) & 31] = x0.z; ring[(q + 3) & 31] = x0.w;
+        ring[(q + 4) & 31] = x1.x; ring[(q + 5) & 31] = x1.y; ring[(q + 6) & 31] = x1.z; ring[(q + 7) & 31] = x1.w;
+        ring[(q + 8) & 31] = x2.x; ring[(q + 9) & 31] = x2.y; ring[(q + 10) & 31] = x2.z; ring[(q + 11) & 31] = x2.w;
+        ring[(q + 12) & 31] = x3.x; ring[(q + 13) & 31] = x3.y; ring[(q + 14) & 31] = x3.z; ring[(q + 15) & 31] = x3.w;
+        br.wp = q + 16;
+        br.nx = ring[q & 31];
+        ldn = false;  // a refill issued before the header is stale
+      }
     } else if (state == S_HUFF) {
       // --- one literal/length symbol (+ its distance) per step
-      br.refill();
+      br.refill_ring(ring);
       int L1;
       bool v1;
       const int i1 = canon_decode(lc, br.bb, L1, v1);
@@ -415,15 +567,15 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
       } else {
         br.drop(L1);
         if (sym < 256) {
-          to.put((uint32_t)sym);
+          if (!tok_put(to, (uint32_t)sym, pool, pool_next, npages)) err = INF_OVERFLOW;
           o++;
-          if (o == us) state = S_DONE;
+          if (o == us || err != INF_OK) state = S_DONE;
         } else if (sym == 256) {
           if (fin) {
             err = INF_SHORT;  // stream end before ISIZE bytes
             state = S_DONE;
           } else {
-            state = S_HDR;
+            state = S_PARK;
           }
         } else {
           const int k = sym - 257;
@@ -435,7 +587,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
           } else {
             const int len = lb + (int)br.peek(lx);
             br.drop(lx);
-            br.refill();
+            br.refill_ring(ring);
             int L2;
             bool v2;
             const int i2 = canon_decode(dc, br.bb, L2, v2);
@@ -460,15 +612,13 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
                   err = INF_DATA;  // invalid distance too far back
                   state = S_DONE;
                 } else {
-                  if (to.n == 7) to.put(kTokPad);
-                  if (to.n == 8 && !tok_flush(to, pool, pool_next, npages)) {
-                    err = INF_OVERFLOW;
-                    state = S_DONE;
-                  }
-                  to.put((uint32_t)(len + 253));
-                  to.put((uint32_t)(dist - 1));
+                  bool ok = true;
+                  if (to.n == 7) ok = tok_put(to, kTokPad, pool, pool_next, npages);  // a match never straddles
+                  ok = ok && tok_put(to, (uint32_t)(len + 253), pool, pool_next, npages);
+                  ok = ok && tok_put(to, (uint32_t)(dist - 1), pool, pool_next, npages);
+                  if (!ok) err = INF_OVERFLOW;
                   o = min(o + len, us);
-                  if (o == us) state = S_DONE;
+                  if (o == us || err != INF_OK) state = S_DONE;
                 }
               }
             }
@@ -476,15 +626,14 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
         }
       }
     } else if (state == S_STORED) {
-      // --- up to 4 stored bytes per step (byte-aligned: bb's low bits are the next byte)
-      br.refill();
-      const int n = min(min(sleft, 4), us - o);
+      // --- up to 2 stored bytes per step (byte-aligned: bb's low bits are the next byte)
+      br.refill_ring(ring);
+      const int n = min(min(sleft, 2), us - o);
       int m = 0;
-      for (int i = 0; i < 4; i++) {
-        if (i < n && br.left >= 8) {
-          to.put(br.peek(8));
+      for (int i = 0; i < 2; i++) {
+        if (i < n && br.left >= 8 && err == INF_OK) {
+          if (!tok_put(to, br.peek(8), pool, pool_next, npages)) err = INF_OVERFLOW;
           br.drop(8);
-          if (to.n == 8 && !tok_flush(to, pool, pool_next, npages)) err = INF_OVERFLOW;
           m++;
         }
       }
@@ -501,32 +650,41 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
           err = INF_SHORT;
           state = S_DONE;
         } else {
-          state = S_HDR;
+          state = S_PARK;
         }
       }
     }
-    if (state != S_DONE && state != S_EXIT && state != S_NEXT && to.n == 8 &&
-        !tok_flush(to, pool, pool_next, npages)) {
-      err = INF_OVERFLOW;
-      state = S_DONE;
-    }
+#ifdef SBAM_DEC_STATS
+    DSTAT_MARK(any_hdr_ ? 2 : 3);
+    DSTAT_ADD(6, any_hdr_ ? 1 : 0);
+#endif
     if (state == S_DONE) {
-      if (to.n > 0 && err != INF_OVERFLOW) {
-        while (to.n < 8) to.put(kTokPad);
-        *reinterpret_cast<uint4 *>(pool + to.cur) = make_uint4(to.t0, to.t1, to.t2, to.t3);
-        to.n = 0;
+      if (err != INF_OVERFLOW) {  // final (padded) chunk and any pending one leave now
+        bool ok = true;
+        if (to.n > 0)
+          while (ok && to.n > 0) ok = tok_put(to, kTokPad, pool, pool_next, npages);
+        if (ok && to.pend) ok = tok_store(to, to.p0, to.p1, to.p2, to.p3, pool, pool_next, npages);
+        if (!ok) err = INF_OVERFLOW;
       }
       to.n = 0;
+      to.pend = false;
+      ldn = false;
       status[blk] = err;
       found[blk] = err == INF_OVERFLOW ? 0 : o;  // an overflowed block has no complete token stream
       state = S_NEXT;
     }
+    DSTAT_MARK(4);
   }
+#ifdef SBAM_DEC_STATS
+  ds_[9] = __builtin_amdgcn_s_memtime() - dt0_;
+  if (__lane_id() == 0)
+    for (int i = 0; i < 10; i++) atomicAdd(&g_dec_stats[i], (unsigned long long)ds_[i]);
+#endif
 }
 
 // ---- resolve kernel -------------------------------------------------------------------------------------------
 constexpr int kResThreads = 256;
-constexpr int kRing = 72;     // per-lane ring stride (64 B used): 18 dwords ⇒ ≤2-way bank conflicts, 8-B aligned
+constexpr int kResRing = 72;     // per-lane ring stride (64 B used): 18 dwords ⇒ ≤2-way bank conflicts, 8-B aligned
 constexpr int kNear = 40;     // copies with (effective) distance <= kNear read the ring
 
 struct TokIn {
@@ -559,17 +717,20 @@ struct TokIn {
   }
 };
 
-__global__ __launch_bounds__(kResThreads, 8) void k_inflate_resolve(BlockTable bt, uint8_t *out,
+__global__ __launch_bounds__(kResThreads, 8) void k_inflate_resolve(BlockTable bt, uint8_t *__restrict__ out,
                                                                     const uint8_t *__restrict__ pool,
                                                                     const int32_t *__restrict__ blk_page,
                                                                     const int32_t *__restrict__ found,
                                                                     unsigned int *next_block) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_ring[kResThreads * kRing];
-  uint8_t *ring = s_ring + threadIdx.x * kRing;
+  __shared__ __attribute__((aligned(16))) uint8_t s_ring[kResThreads * kResRing];
+  uint8_t *ring = s_ring + threadIdx.x * kResRing;
   uint32_t *ring32 = reinterpret_cast<uint32_t *>(ring);
+  const uint32_t *out32 = reinterpret_cast<const uint32_t *>(out);
 
+  // positions are byte offsets into `out` (kept as offsets so every access stays a global, not flat, access;
+  // `out` is 256-B aligned, so offset alignment is address alignment)
   bool active = false, exited = false;
-  uint8_t *a = nullptr, *ae = nullptr, *fl = nullptr;
+  int64_t a = 0, ae = 0, fl = 0;
   TokIn ti{0, 0, 0, 0, 0, 0, 0};
   int crem = 0, eff = 0, npad = 0;
 
@@ -582,7 +743,7 @@ __global__ __launch_bounds__(kResThreads, 8) void k_inflate_resolve(BlockTable b
         const int32_t f = found[b];
         const int32_t pg = blk_page[b];
         if (f > 0 && pg >= 0) {
-          a = out + bt.uoff[b];
+          a = bt.uoff[b];
           ae = a + f;
           fl = a;
           ti.n = 0;
@@ -599,7 +760,7 @@ __global__ __launch_bounds__(kResThreads, 8) void k_inflate_resolve(BlockTable b
     if (crem == 0) {
       const uint32_t t = ti.get(pool);
       if (t < 256) {
-        ring[reinterpret_cast<uintptr_t>(a) & 63] = (uint8_t)t;
+        ring[a & 63] = (uint8_t)t;
         a++;
       } else if (t != kTokPad) {
         crem = (int)t - 253;
@@ -610,7 +771,7 @@ __global__ __launch_bounds__(kResThreads, 8) void k_inflate_resolve(BlockTable b
     }
     if (crem > 0) {
       const int n = min(min(crem, 16), min(eff, (int)(ae - a)));
-      const uintptr_t src = reinterpret_cast<uintptr_t>(a) - (uintptr_t)eff;
+      const int64_t src = a - eff;
       uint32_t v0, v1, v2, v3;
       const int sh = (int)(src & 3);
       if (eff <= kNear) {  // source in the ring: 5 dwords around it
@@ -622,7 +783,7 @@ __global__ __launch_bounds__(kResThreads, 8) void k_inflate_resolve(BlockTable b
         v2 = __builtin_amdgcn_alignbyte(s3, s2, sh);
         v3 = __builtin_amdgcn_alignbyte(s4, s3, sh);
       } else {  // source already stored to HBM (it lies below the flushed mark)
-        const uint32_t *g = reinterpret_cast<const uint32_t *>(src & ~(uintptr_t)3);
+        const uint32_t *g = out32 + (src >> 2);
         const uint4 x = *reinterpret_cast<const uint4 *>(g);
         const uint32_t x4 = g[4];
         v0 = __builtin_amdgcn_alignbyte(x.y, x.x, sh);
@@ -632,14 +793,13 @@ __global__ __launch_bounds__(kResThreads, 8) void k_inflate_resolve(BlockTable b
       }
       // write 16 bytes at a (bytes past a + n are scratch, rewritten before they are flushed):
       // head bytes up to the next dword boundary, then 4 aligned dwords
-      const uintptr_t aa = reinterpret_cast<uintptr_t>(a);
-      const int h = (int)((4 - (aa & 3)) & 3);
+      const int h = (int)((4 - (a & 3)) & 3);
 #pragma unroll
       for (int k = 0; k < 3; k++)
-        if (k < h) ring[(aa + k) & 63] = (uint8_t)(v0 >> (8 * k));
+        if (k < h) ring[(a + k) & 63] = (uint8_t)(v0 >> (8 * k));
       const uint32_t w0 = __builtin_amdgcn_alignbyte(v1, v0, h), w1 = __builtin_amdgcn_alignbyte(v2, v1, h),
                      w2 = __builtin_amdgcn_alignbyte(v3, v2, h), w3 = __builtin_amdgcn_alignbyte(0u, v3, h);
-      const int q = (int)(((aa + h) & 63) >> 2);
+      const int q = (int)(((a + h) & 63) >> 2);
       ring32[q & 15] = w0;
       ring32[(q + 1) & 15] = w1;
       ring32[(q + 2) & 15] = w2;
@@ -649,27 +809,24 @@ __global__ __launch_bounds__(kResThreads, 8) void k_inflate_resolve(BlockTable b
       if (n == eff && eff < 16) eff *= 2;  // the copied bytes extend the period: distance 2·eff is valid
     }
     // flush: a block's partial first chunk (shared with the previous block) as bytes, then aligned 16-B chunks
-    {
-      const uintptr_t f = reinterpret_cast<uintptr_t>(fl);
-      if (f & 15) {
-        const uintptr_t hd = (f & ~(uintptr_t)15) + 16;
-        if (reinterpret_cast<uintptr_t>(a) >= hd || a == ae) {
-          const uintptr_t lim = reinterpret_cast<uintptr_t>(a) < hd ? reinterpret_cast<uintptr_t>(a) : hd;
-          for (uintptr_t x = f; x < lim; x++) *reinterpret_cast<uint8_t *>(x) = ring[x & 63];
-          fl = reinterpret_cast<uint8_t *>(lim);
-        }
+    if (fl & 15) {
+      const int64_t hd = (fl & ~(int64_t)15) + 16;
+      if (a >= hd || a == ae) {
+        const int64_t lim = a < hd ? a : hd;
+        for (int64_t x = fl; x < lim; x++) out[x] = ring[x & 63];
+        fl = lim;
       }
-      while ((reinterpret_cast<uintptr_t>(fl) & 15) == 0 && a - fl >= 16) {
-        const uint2 lo = *reinterpret_cast<const uint2 *>(ring + (reinterpret_cast<uintptr_t>(fl) & 63));
-        const uint2 hi = *reinterpret_cast<const uint2 *>(ring + ((reinterpret_cast<uintptr_t>(fl) + 8) & 63));
-        *reinterpret_cast<uint4 *>(fl) = make_uint4(lo.x, lo.y, hi.x, hi.y);
-        fl += 16;
-      }
-      if (a == ae) {  // tail (shared with the next block) as bytes
-        for (uint8_t *x = fl; x < ae; x++) *x = ring[reinterpret_cast<uintptr_t>(x) & 63];
-        fl = ae;
-        active = false;
-      }
+    }
+    while ((fl & 15) == 0 && a - fl >= 16) {
+      const uint2 lo = *reinterpret_cast<const uint2 *>(ring + (fl & 63));
+      const uint2 hi = *reinterpret_cast<const uint2 *>(ring + ((fl + 8) & 63));
+      *reinterpret_cast<uint4 *>(out + fl) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      fl += 16;
+    }
+    if (a == ae) {  // tail (shared with the next block) as bytes
+      for (int64_t x = fl; x < ae; x++) out[x] = ring[x & 63];
+      fl = ae;
+      active = false;
     }
   }
 }
@@ -685,16 +842,31 @@ hipError_t launch_first_error(const int32_t *status, int64_t n, unsigned long lo
   return hipGetLastError();
 }
 
-hipError_t launch_inflate_tokens(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *out, uint8_t *pool,
-                                 uint32_t npages, int32_t *blk_page, int32_t *status, int32_t *found,
-                                 unsigned int *counters, int dec_wgs, int res_wgs, hipStream_t s) {
+#ifdef SBAM_DEC_STATS
+extern "C" int sbam_debug_decode_stats(unsigned long long *out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dec_stats), sizeof(g_dec_stats)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dec_stats), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
+
+hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *pool, uint32_t npages,
+                                 int32_t *blk_page, int32_t *status, int32_t *found, unsigned int *counters,
+                                 int dec_wgs, hipStream_t s) {
   if (bt.n == 0) return hipSuccess;
   // counters: [0] decode work, [1] pool pages used, [2] resolve work
   (void)hipMemsetAsync(counters, 0, 3 * sizeof(unsigned int), s);
   hipLaunchKernelGGL(k_inflate_decode, dim3((unsigned)dec_wgs), dim3(kDecThreads), 0, s, d, D, bt, pool, npages,
                      counters + 1, blk_page, status, found, counters + 0);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  return hipGetLastError();
+}
+
+hipError_t launch_inflate_resolve(BlockTable bt, uint8_t *out, const uint8_t *pool, const int32_t *blk_page,
+                                  const int32_t *found, unsigned int *counters, int res_wgs, hipStream_t s) {
+  if (bt.n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_inflate_resolve, dim3((unsigned)res_wgs), dim3(kResThreads), 0, s, bt, out, pool, blk_page,
                      found, counters + 2);
   return hipGetLastError();

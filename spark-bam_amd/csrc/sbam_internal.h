@@ -47,7 +47,7 @@ struct CountsDev {  // mirrors sbam_counts (int64 fields) in device memory
 constexpr int kScanChunk = 1 << 20;  // bytes per workgroup in the BGZF candidate scan
 constexpr int kInflateScratchU16 = 2048;  // per-lane Huffman table scratch (u16 entries)
 constexpr int kStreamPad = 16384;  // zero pad behind the uncompressed stream (>= checker LDS window)
-constexpr int kCompPad = 64;  // zero pad behind the compressed bytes (bit-reader lookahead)
+constexpr int kCompPad = 256;  // zero pad behind the compressed bytes (bit-reader / input-ring lookahead)
 constexpr uint64_t kTokPage = 4096;  // inflate token page: 16-B header (next page) + 255 chunks of 8 u16 tokens
 
 hipError_t launch_scan_count(const uint8_t *d, int64_t D, int32_t *chunk_counts, int64_t nchunks, hipStream_t s);
@@ -66,10 +66,12 @@ hipError_t launch_inflate(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *o
                           int32_t *status, int32_t *found, unsigned int *next_block, unsigned long long *first_err,
                           hipStream_t s);
 // Two-kernel inflate (sbam_inflate.hip): entropy decode into token pages, then LZ77 resolve into `out`.
-// counters: 3 × u32 device scratch (decode work, pool pages used, resolve work).
-hipError_t launch_inflate_tokens(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *out, uint8_t *pool,
-                                 uint32_t npages, int32_t *blk_page, int32_t *status, int32_t *found,
-                                 unsigned int *counters, int dec_wgs, int res_wgs, hipStream_t s);
+// counters: 3 × u32 device scratch (decode work, pool pages used, resolve work), reset by the decode launch.
+hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *pool, uint32_t npages,
+                                 int32_t *blk_page, int32_t *status, int32_t *found, unsigned int *counters,
+                                 int dec_wgs, hipStream_t s);
+hipError_t launch_inflate_resolve(BlockTable bt, uint8_t *out, const uint8_t *pool, const int32_t *blk_page,
+                                  const int32_t *found, unsigned int *counters, int res_wgs, hipStream_t s);
 // first_err = min block index with status != 0 (caller presets ~0)
 hipError_t launch_first_error(const int32_t *status, int64_t n, unsigned long long *first_err, hipStream_t s);
 hipError_t launch_lower_bound(const Candidate *c, int64_t n, int64_t q, int64_t *out, hipStream_t s);

@@ -45,13 +45,13 @@ def main():
             f.reset()
             f.run(contig_lengths=s.contig_lengths)
         scan_inflate()
-        tt = {"scan": [], "inflate": []}
+        tt = {"scan": [], "inflate": [], "inflate_decode": [], "inflate_resolve": []}
         for _ in range(args.reps):
             scan_inflate()
-            tt["scan"].append(f.kernel_ms("scan"))
-            tt["inflate"].append(f.kernel_ms("inflate"))
-        ms["scan"] = round(float(np.median(tt["scan"])), 3)
-        ms["inflate"] = round(float(np.median(tt["inflate"])), 3)
+            for k in tt:
+                tt[k].append(f.kernel_ms(k))
+        for k in tt:
+            ms[k] = round(float(np.median(tt[k])), 3)
     if "check_full" in only:
         timed("check_full", lambda: f.check_full_counts(0, U), "check_full")
         c = f.check_full_counts(0, U)
