@@ -32,7 +32,8 @@ constexpr int kCheckThreads = 256;
 constexpr int kTile = 8192;                 // positions per tile (64-aligned tile bases)
 constexpr int kHalo = 768;                  // staged bytes past the tile (fixed fields + 255-B name + ops)
 constexpr int kWin = kTile + kHalo;         // staged window (multiple of 16)
-constexpr int kInvWords = kWin / 32 + 4;    // bitmap words (+ pad for 64-bit extraction)
+constexpr int kOpcWords = kWin / 128 + 4;   // per residue class: one bit per 4 window bytes (+ pad)
+constexpr int kNameWords = kWin / 32 + 4;   // one bit per window byte (+ pad)
 constexpr int kLdsLens = 4096;              // contig lengths kept in LDS when n_ref fits
 constexpr int kFlushTiles = 7;              // 7 tiles x 32 positions per lane < 255 (8-bit planes / counters)
 static_assert(kWin % 16 == 0, "window");
@@ -268,24 +269,21 @@ __global__ __launch_bounds__(256) void k_chains(StreamView sv, int64_t x0, int64
 }
 
 // ---- first record against the LDS window --------------------------------------------------------------------
-struct Tile {
-  const uint8_t *win;   // staged bytes: win[r] = u[base + r], r < kWin
-  const uint32_t *inv;  // bit r: (win[r] & 0xf) > 8
-  int64_t base;
-};
+// Global (address space 1) view of the stream: pointers that arrive inside a kernel-argument struct are generic,
+// and generic (flat) loads make every later LDS wait also wait for them.
+typedef const __attribute__((address_space(1))) uint8_t *gbytes;
+SB_DEV gbytes gview(const uint8_t *p) { return (gbytes)p; }
 
-SB_DEV uint32_t byte_at(const Tile &t, const StreamView &sv, int64_t x) {
-  const int64_t r = x - t.base;
-  return r < kWin ? (uint32_t)t.win[r] : (uint32_t)sv.u[x];
-}
-struct TileBytes {  // the staged window where it covers x, else global memory
-  const uint8_t *win;
+// The staged tile: bytes, plus two bitmaps built while staging —
+//   opc[r] (r = 0..3): bit k = "(win[4k + r] & 0xf) > 8", i.e. CIGAR op k of any op array starting at a byte
+//     offset ≡ r (mod 4) is invalid (Checker.MAX_CIGAR_OP; only an op's first byte matters): one 64-bit read
+//     covers 64 consecutive ops;
+//   nbad: bit r = "win[r] is not an allowed read-name character" (Checker.allowedReadNameChars).
+struct Tile {
+  const uint8_t *win;     // staged bytes: win[r] = u[base + r], r < kWin
+  const uint32_t *opc;    // 4 × kOpcWords dwords
+  const uint32_t *nbad;   // kNameWords dwords
   int64_t base;
-  const uint8_t *u;
-  SB_DEV uint32_t operator()(int64_t x) const {
-    const int64_t r = x - base;
-    return r < kWin ? (uint32_t)win[r] : (uint32_t)u[x];
-  }
 };
 
 SB_DEV uint64_t bits64(const uint32_t *bm, int x) {
@@ -295,97 +293,106 @@ SB_DEV uint64_t bits64(const uint32_t *bm, int x) {
   return s ? (lo >> s) | (hi << (64 - s)) : lo;
 }
 
-// Any byte of [c, c+n) outside allowedReadNameChars?  SWAR over aligned window dwords.
-SB_DEV bool name_has_bad(const Tile &t, const StreamView &sv, int64_t c, int32_t n) {
-  if (n <= 0) return false;
-  const int64_t rel = c - t.base;
-  if (rel + n <= kWin) {
-    const uint32_t *w32 = reinterpret_cast<const uint32_t *>(t.win);
-    const int r0 = (int)rel, r1 = (int)rel + n;
-    for (int d = r0 & ~3; d < r1; d += 4) {
-      uint32_t w = w32[d >> 2];
-      const int lo = r0 > d ? r0 - d : 0, hi = r1 - d < 4 ? r1 - d : 4;
-      const uint32_t keep = (uint32_t)((0xffffffffull << (8 * lo)) & ((1ull << (8 * hi)) - 1));
-      w = (w & keep) | (0x41414141u & ~keep);
-      if (name_bad_bytes(w)) return true;
-    }
-    return false;
-  }
-  for (int32_t i = 0; i < n; i++) {
-    const uint32_t b = sv.u[c + i];
-    if (!((b - 33u <= 30u) || (b - 65u <= 61u))) return true;
+// Any byte of the name body [rel, rel + n) outside allowedReadNameChars? (n <= 254, inside the window)
+SB_DEV bool name_has_bad(const Tile &t, int rel, int32_t n) {
+  for (int32_t o = 0; o < n; o += 64) {
+    uint64_t m = bits64(t.nbad, rel + o);
+    if (n - o < 64) m &= (1ull << (n - o)) - 1ull;
+    if (m) return true;
   }
   return false;
 }
 
 // Index of the first op among the first `lim` ops at c, c+4, ... whose first byte has (b & 0xf) > 8, or lim.
 SB_DEV int32_t first_bad_op(const Tile &t, const StreamView &sv, int64_t c, int32_t lim) {
-  const int64_t rel = c - t.base;
-  const int32_t nwin = rel < kWin ? (int32_t)((kWin - rel + 3) >> 2) : 0;
-  const int32_t n1 = lim < nwin ? lim : nwin;
-  for (int32_t i = 0; i < n1; i += 16) {
-    uint64_t m = bits64(t.inv, (int)rel + 4 * i) & 0x1111111111111111ull;
-    const int32_t rem = n1 - i;
-    if (rem < 16) m &= (1ull << (4 * rem)) - 1ull;
-    if (m) return i + (int32_t)(__builtin_ctzll(m) >> 2);
+  const int rel = (int)(c - t.base);
+  const uint64_t m = bits64(t.opc + (rel & 3) * kOpcWords, rel >> 2);
+  if (m) {
+    const int32_t b = (int32_t)__builtin_ctzll(m);
+    return b < lim ? b : lim;
   }
-  for (int32_t i = n1; i < lim; i++)
-    if ((sv.u[c + 4 * (int64_t)i] & 0xfu) > 8u) return i;
+  if (lim <= 64) return lim;
+  const gbytes u = gview(sv.u);  // > 64 valid ops in a row: rare, read on from HBM
+  for (int32_t i = 64; i < lim; i++)
+    if ((u[c + 4 * (int64_t)i] & 0xfu) > 8u) return i;
   return lim;
 }
 
+// PosChecker.getRefPosError bits with the contig length read unconditionally (clamped index) from LDS.
+SB_DEV uint32_t ref_bits_lds(int32_t ri, int32_t rp, const int32_t *lensL, int32_t nref) {
+  const bool in = (uint32_t)ri < (uint32_t)nref;
+  const int32_t len = lensL[in ? ri : 0];
+  return (ri < -1 ? 1u : 0u) | (ri >= nref ? 2u : 0u) | (rp < -1 ? 4u : 0u) | (in && rp > len ? 8u : 0u);
+}
+
+// Record 0 at x (full.Checker.scala:22-184 / eager.Checker.scala:24-126 for k = 0), fixed fields in f[],
+// rel = x - tile base.  Every check is evaluated unconditionally from the tile (clamped LDS reads, no
+// per-lane branches) so a wave's lanes cost the same; only the rare tails (a name body or an op array
+// running past 64 checked bytes / ops) branch out to HBM.
 template <bool EAGER>
-SB_DEV uint32_t check_first(const Tile &t, const StreamView &sv, const int32_t *lensL, int64_t x, int R,
+SB_DEV uint32_t check_first(const Tile &t, const StreamView &sv, const int32_t *lensL, int64_t x, int rel, int R,
                             const int32_t f[8]) {
   if (R == 0) return W_PASS0;  // Success(0): resolved by the chain pass
-  if (x + 36 > sv.L) return sv.eof_real ? 1u : W_HALO;
   const int32_t bs = f[0], ri = f[1], rp = f[2], bmn = f[3], fnc = f[4], ls = f[5], nri = f[6], nrp = f[7];
-  uint32_t F = ref_err(ri, rp, lensL, sv.lens, sv.nref) << 1;
   const int32_t lrn = bmn & 0xff;
   const uint32_t flag = ((uint32_t)fnc) >> 16;
   const int32_t nc = fnc & 0xffff;
-  F |= too_few_remaining(bs, lrn, nc, ls) ? (1u << 18) : 0u;
-  F |= ref_err(nri, nrp, lensL, sv.lens, sv.nref) << 5;
+  const uint32_t rb0 = lensL ? ref_bits_lds(ri, rp, lensL, sv.nref) : ref_err(ri, rp, nullptr, sv.lens, sv.nref);
+  const uint32_t rb1 = lensL ? ref_bits_lds(nri, nrp, lensL, sv.nref) : ref_err(nri, nrp, nullptr, sv.lens, sv.nref);
+  const uint32_t Fref = (rb0 << 1) | (rb1 << 5) | (too_few_remaining(bs, lrn, nc, ls) ? (1u << 18) : 0u);
   const bool empty_mapped = (flag & 4u) == 0 && (ls == 0 || nc == 0);
-  if (EAGER && (F || lrn < 2 || empty_mapped)) return F ? F : (1u << 12);
-#if SBAM_ABLATE == 1  // timing experiment only: fixed-field checks alone
-  return F | (1u << 15);
-#endif
-  int64_t c = x + 36;
-  if (lrn < 2) {
-    F |= lrn == 0 ? (1u << 12) : (1u << 13);
+  if (EAGER && x + 36 <= sv.L && (Fref || lrn < 2 || empty_mapped))
+    return Fref ? Fref : (1u << 12);  // eager: ~96 % of positions end here, skip the rest of the record
+  // read name: lrn 0/1 → noReadName / emptyReadName (name not consumed); else last byte NUL, then characters
+  const bool has_name = lrn >= 2;
+  const bool name_eof = has_name && x + 36 + lrn > sv.L;
+  const uint32_t last = t.win[rel + 35 + (has_name ? lrn : 1)];
+  const bool nonnull = has_name && last != 0;
+  const bool scan = has_name && last == 0;
+  const int32_t nbody = lrn - 1;
+  uint64_t nbm = bits64(t.nbad, rel + 36);
+  if (nbody < 64) nbm &= (1ull << (nbody > 0 ? nbody : 0)) - 1ull;
+  bool nonascii = scan && nbm != 0;
+  if (scan && nbm == 0 && nbody > 64 && !name_eof) nonascii = name_has_bad(t, rel + 36 + 64, nbody - 64);
+  // CIGAR ops: the first invalid op among min(n_cigar, ops before EOF)
+  const int32_t clen = has_name ? lrn : 0;
+  const int64_t c = x + 36 + clen;
+  const int crel = rel + 36 + clen;
+  const int64_t n_eof64 = (sv.L - c) >> 2;
+  const int32_t n_eof = n_eof64 < 0 ? 0 : n_eof64 > 0x7fffffff ? 0x7fffffff : (int32_t)n_eof64;
+  const int32_t lim = n_eof < nc ? n_eof : nc;
+  const uint64_t om = bits64(t.opc + (crel & 3) * kOpcWords, crel >> 2);
+  int32_t bad = om ? (int32_t)__builtin_ctzll(om) : 64;
+  if (om == 0 && lim > 64 && !name_eof) bad = first_bad_op(t, sv, c, lim);
+  const bool inv_op = nc > 0 && bad < lim;
+  const bool few_ops = nc > 0 && !inv_op && n_eof < nc;
+  uint32_t F = Fref;
+  F |= lrn == 0 ? (1u << 12) : 0u;
+  F |= lrn == 1 ? (1u << 13) : 0u;
+  F |= nonnull ? (1u << 10) : 0u;
+  F |= nonascii ? (1u << 11) : 0u;
+  F |= inv_op ? (1u << 15) : 0u;
+  F |= few_ops ? (1u << 14) : 0u;
+  F |= (empty_mapped && !inv_op && !few_ops) ? (((ls == 0) ? (1u << 16) : 0u) | ((nc == 0) ? (1u << 17) : 0u)) : 0u;
+  // result, in the reference's order of early exits
+  const bool fixed_eof = x + 36 > sv.L;
+  uint32_t w;
+  if (EAGER) {  // eager.Checker: false at the first failing group (only pass/fail and HALO matter)
+    const bool fail_fixed = Fref || !has_name || empty_mapped;
+    const bool fail_name = nonnull || nonascii;
+    w = fixed_eof ? (sv.eof_real ? 1u : W_HALO)
+        : fail_fixed ? (Fref ? Fref : (1u << 12))
+        : name_eof ? (sv.eof_real ? (1u << 9) : W_HALO)
+        : fail_name ? F
+        : (few_ops && !sv.eof_real) ? W_HALO
+        : F ? F : W_PASS0;
   } else {
-    if (c + lrn > sv.L) return sv.eof_real ? (F | (1u << 9)) : W_HALO;
-    if (byte_at(t, sv, c + lrn - 1) != 0) F |= 1u << 10;
-    else if (name_has_bad(t, sv, c, lrn - 1)) F |= 1u << 11;
-    c += lrn;
-    if (EAGER && F) return F;
+    w = fixed_eof ? (sv.eof_real ? 1u : W_HALO)
+        : name_eof ? (sv.eof_real ? (Fref | (1u << 9)) : W_HALO)
+        : (few_ops && !sv.eof_real) ? W_HALO
+        : F ? F : W_PASS0;  // record 0 passed: the 10-record chain is resolved by k_chains
   }
-  bool cig_err = false;
-#if SBAM_ABLATE == 2  // timing experiment only: no CIGAR scan
-  return F | (1u << 15);
-#endif
-  if (nc > 0) {
-    const int64_t n_eof = (sv.L - c) >> 2;  // ops readable before EOF (c <= L here)
-    const int32_t lim = n_eof < nc ? (int32_t)n_eof : nc;
-    const int32_t bad = first_bad_op(t, sv, c, lim);
-    if (bad < lim) {
-      F |= 1u << 15;
-      cig_err = true;
-    } else if (n_eof < nc) {
-      if (!sv.eof_real) return W_HALO;
-      F |= 1u << 14;
-      cig_err = true;
-    }
-  }
-  if (!cig_err && empty_mapped) {
-    F |= (ls == 0) ? (1u << 16) : 0u;
-    F |= (nc == 0) ? (1u << 17) : 0u;
-  }
-  if (F) return F;
-  // record 0 passed (true starts and rare near-misses): the 10-record chain is resolved after the tile's
-  // positions, one candidate per lane, so it never stalls a whole wave-step (k_check, deferred pass)
-  return W_PASS0;
+  return w;
 }
 
 // ---- the tiled kernel -------------------------------------------------------------------------------------
@@ -426,9 +433,13 @@ struct Acc {
     keyc[0] = keyc[1] = keyc[2] = 0;
     n_succ = n_tff = n_halo = 0;
   }
-  // classify w; returns the counted flag word F (0 if not counted); rare per-key paths go to global atomics
+  // classify w; returns the counted flag word F (0 if not counted).  The rare per-key paths (keys 1-2 per flag,
+  // close-call pairs) count into the workgroup's LDS tables k12 / pair; only readsBeforeError (kk > 0, chains
+  // only) goes straight to global atomics.  (Global atomics from every workgroup onto the same few hundred
+  // counters serialise at the memory side: 0.3 % of positions made them the checker's bottleneck.)
   template <bool BYKEY>
-  SB_DEV uint32_t classify(uint32_t w, const CountsDev &cd, uint32_t &key_out, bool &counted_out) {
+  SB_DEV uint32_t classify(uint32_t w, const CountsDev &cd, uint32_t *k12, uint32_t *pair, uint32_t &key_out,
+                           bool &counted_out) {
     const bool succ = (w & W_SUCC) != 0;
     const bool halo = w == W_HALO;
     const bool tff = w == 1u;
@@ -446,10 +457,10 @@ struct Acc {
       keyc[2] += (key >> 3) == 2 ? inc : 0ull;
       if (key <= 2 || kk > 0) {  // rare: keys 1-2 per flag, close-call pairs, readsBeforeError histogram
         if (!BYKEY && key <= 2)
-          for (uint32_t m = F; m; m &= m - 1) atomicAdd(&cd.counts[key * 19 + __builtin_ctz(m)], 1ull);
+          for (uint32_t m = F; m; m &= m - 1) atomicAdd(&k12[key * 19 + __builtin_ctz(m)], 1u);
         if (key == 2) {
           const uint32_t fi = __builtin_ctz(F), rest = F & (F - 1);
-          atomicAdd(&cd.pair[fi * 19 + (rest ? __builtin_ctz(rest) : fi)], 1ull);
+          atomicAdd(&pair[fi * 19 + (rest ? __builtin_ctz(rest) : fi)], 1u);
         }
         if (kk > 0) atomicAdd(&cd.rbe[key * 128 + kk], 1ull);
       }
@@ -508,11 +519,16 @@ __global__ __launch_bounds__(kCheckThreads) void k_check(StreamView sv, int64_t 
   constexpr bool COUNTS = MODE == MODE_COUNTS || MODE == MODE_BYKEY;
   constexpr bool BYKEY = MODE == MODE_BYKEY;
   __shared__ __attribute__((aligned(16))) uint8_t s_win[kWin + 64];
-  __shared__ uint32_t s_inv[kInvWords];
+  __shared__ uint32_t s_opc[4 * kOpcWords];
+  __shared__ uint32_t s_nbad[kNameWords];
   __shared__ int32_t s_lens[kLdsLens];
   __shared__ unsigned long long s_acc[19 + 21 + 3];  // totals, positions per key, succ/tff/halo
   __shared__ uint32_t s_cnt[BYKEY ? 21 * 19 : 1];
+  __shared__ uint32_t s_k12[3 * 19];    // keys 0-2 × flag (non-BYKEY modes)
+  __shared__ uint32_t s_pair[19 * 19];  // close-call pairs (key 2)
   const int lane = lane_id();
+  for (int i = threadIdx.x; i < 3 * 19; i += kCheckThreads) s_k12[i] = 0;
+  for (int i = threadIdx.x; i < 19 * 19; i += kCheckThreads) s_pair[i] = 0;
   const int32_t *lensL = nullptr;
   if (sv.nref <= kLdsLens) {
     for (int i = threadIdx.x; i < sv.nref; i += kCheckThreads) s_lens[i] = (int32_t)sv.lens[i];
@@ -531,19 +547,35 @@ __global__ __launch_bounds__(kCheckThreads) void k_check(StreamView sv, int64_t 
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int64_t base = x0a + t * kTile;
     __syncthreads();
-    {  // stage the window and build the op-validity bitmap (16 bytes per lane per step)
-      const uint4 *src = reinterpret_cast<const uint4 *>(sv.u + base);
-      uint4 *dst = reinterpret_cast<uint4 *>(s_win);
-      uint16_t *inv16 = reinterpret_cast<uint16_t *>(s_inv);
-      for (int i = threadIdx.x; i < kWin / 16; i += kCheckThreads) {
-        const uint4 v = src[i];
-        dst[i] = v;
-        inv16[i] = (uint16_t)(inv_nibble(v.x) | (inv_nibble(v.y) << 4) | (inv_nibble(v.z) << 8) | (inv_nibble(v.w) << 12));
+    {  // stage the window (32 B per lane per step) and build the op-class and name-character bitmaps
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      typedef const __attribute__((address_space(1))) u32x4 *g16;
+      const g16 src = (g16)(gview(sv.u) + base);
+      u32x4 *dst = reinterpret_cast<u32x4 *>(s_win);
+      uint8_t *opc8 = reinterpret_cast<uint8_t *>(s_opc);
+      for (int i = threadIdx.x; i < kWin / 32; i += kCheckThreads) {
+        const u32x4 a = src[2 * i], b = src[2 * i + 1];
+        dst[2 * i] = a;
+        dst[2 * i + 1] = b;
+        const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint32_t cls[4] = {0, 0, 0, 0}, nb = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const uint32_t inv = inv_nibble(w[j]);  // bit r: byte r of w[j] is an invalid op start
+#pragma unroll
+          for (int r = 0; r < 4; r++) cls[r] |= ((inv >> r) & 1u) << j;
+          const uint32_t m = name_bad_bytes(w[j]);  // bit 7 of each bad byte
+          nb |= (((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u)) << (4 * j);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) opc8[r * 4 * kOpcWords + i] = (uint8_t)cls[r];
+        s_nbad[i] = nb;
       }
-      if (threadIdx.x < 4) s_inv[kWin / 32 + threadIdx.x] = 0;
+      if (threadIdx.x < 4) s_nbad[kWin / 32 + threadIdx.x] = 0;
+      if (threadIdx.x < 16) s_opc[(threadIdx.x >> 2) * kOpcWords + kWin / 128 + (threadIdx.x & 3)] = 0;
     }
     __syncthreads();
-    const Tile tl{s_win, s_inv, base};
+    const Tile tl{s_win, s_opc, s_nbad, base};
     const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
 #pragma unroll 1
     for (int j = 0; j < kTile / (4 * kCheckThreads); j++) {
@@ -559,7 +591,8 @@ __global__ __launch_bounds__(kCheckThreads) void k_check(StreamView sv, int64_t 
         int32_t f[8];
 #pragma unroll
         for (int q = 0; q < 8; q++) f[q] = (int32_t)__builtin_amdgcn_alignbyte(W[q + 1], W[q], o);
-        uint32_t w = (x >= x0 && x < x1) ? check_first<EAGER>(tl, sv, lensL, x, R, f) : W_NONE;
+        uint32_t w = check_first<EAGER>(tl, sv, lensL, x, 4 * g + o, R, f);
+        w = (x >= x0 && x < x1) ? w : W_NONE;
         wd[o] = w;
       }
       if (MODE == MODE_WORDS) {
@@ -587,7 +620,8 @@ __global__ __launch_bounds__(kCheckThreads) void k_check(StreamView sv, int64_t 
         uint32_t key = 0;
         bool counted = false;
         Fo[o] = 0;
-        if (wd[o] != W_NONE && wd[o] != W_PASS0) Fo[o] = acc.classify<BYKEY>(wd[o], cd, key, counted);
+        if (wd[o] != W_NONE && wd[o] != W_PASS0)
+          Fo[o] = acc.classify<BYKEY>(wd[o], cd, s_k12, s_pair, key, counted);
         if (BYKEY) bykey_count(s_cnt, lane, counted, key, Fo[o]);
       }
       const uint32_t x1a = Fo[0] ^ Fo[1], c1 = Fo[0] & Fo[1];
@@ -615,6 +649,11 @@ __global__ __launch_bounds__(kCheckThreads) void k_check(StreamView sv, int64_t 
     if (BYKEY)
       for (int i = threadIdx.x; i < 21 * 19; i += kCheckThreads)
         if (s_cnt[i]) atomicAdd(&cd.counts[i], (unsigned long long)s_cnt[i]);
+    if (!BYKEY)
+      for (int i = threadIdx.x; i < 3 * 19; i += kCheckThreads)
+        if (s_k12[i]) atomicAdd(&cd.counts[i], (unsigned long long)s_k12[i]);
+    for (int i = threadIdx.x; i < 19 * 19; i += kCheckThreads)
+      if (s_pair[i]) atomicAdd(&cd.pair[i], (unsigned long long)s_pair[i]);
   }
 }
 

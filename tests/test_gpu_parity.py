@@ -72,6 +72,24 @@ def test_full_counts(name, reads_to_check, by_key, gpu_files, oracle_files):
     assert c.n_success == nsucc
     w = o.check_full_range(0, o.L, reads_to_check)
     assert np.array_equal(bits, (w & 0x80000000) != 0)
+    assert np.array_equal(c.pair_hist, pair_hist(w))
+
+
+def pair_hist(w):
+    """Close-call pairs of the full-check report: key-2 results by (first flag, second flag), or (flag, flag)
+    when the second non-zero field is readsBeforeError (FullCheck.scala:141-191)."""
+    F = (w & 0x7ffff).astype(np.int64)
+    k = (w >> 24) & 0x7f
+    counted = ((w & 0x80000000) == 0) & ~((F == 1) & (k == 0))
+    pop = np.zeros_like(F)
+    for f in range(19):
+        pop += (F >> f) & 1
+    key2 = counted & (pop + (k > 0) == 2)
+    out = np.zeros((19, 19), np.int64)
+    for Fi in F[key2]:
+        bits = [f for f in range(19) if (Fi >> f) & 1]
+        out[bits[0], bits[1] if len(bits) > 1 else bits[0]] += 1
+    return out
 
 
 @pytest.mark.parametrize("name", ["2.bam", "5k.bam"])
