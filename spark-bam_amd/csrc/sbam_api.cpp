@@ -468,7 +468,7 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
     if (c->pool_cap > want) want = c->pool_cap;
     HIPCHK(c, ensure(&c->d_blkpage, &c->blkpage_cap, nb));
     if (!c->d_icnt) HIPCHK(c, dalloc(&c->d_icnt, 4));
-    const int dec_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256);
+    const int dec_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256 * 2);
     const int res_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256 * 8);
     for (;;) {
       if (c->pool_cap < want) {

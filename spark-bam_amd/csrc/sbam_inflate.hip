@@ -34,19 +34,22 @@ enum : int32_t { INF_OK = 0, INF_SHORT = 1, INF_DATA = 2, INF_OVERFLOW = 3 };
 // followed by the token (distance - 1).  0xffff: padding.
 constexpr uint32_t kTokPad = 0xffffu;
 
-// ---- decode kernel: per-lane LDS slice ------------------------------------------------------------------------
+// ---- decode kernel --------------------------------------------------------------------------------------------
+// Per-lane tables live in LDS, interleaved across the workgroup's lanes at dword granularity (byte b of lane L at
+// ((b >> 2) * kDecThreads + L) * 4 + (b & 3)): lanes reading the same table offset never share a bank, and the
+// 320-B slice lets two 256-lane workgroups — two waves per SIMD — share a CU's 160 KiB.  Everything else a lane
+// needs (canonical code limits, the input window, the token chunk) is in VGPRs.
 constexpr int kDecThreads = 256;
-constexpr int kSlice = 580;        // 145 dwords (odd): lanes at the same offset hit different banks
-constexpr int kLitSorted = 0;      // 288 B: lit/len symbols in canonical order (low 8 bits)
-constexpr int kClTab = 0;          //   during a dynamic header: 128-entry code-length-code table (u8: len<<5 | sym)
-constexpr int kLitHi = 288;        // 36 B: bit i set ⇔ canonical entry i is a symbol >= 256
-constexpr int kDistSorted = 324;   // 32 B: distance symbols in canonical order
-constexpr int kCnt = 356;          // 16 × u32: per-length counts, then fill cursors (builds only)
-constexpr int kLens = 420;         // 160 B: code lengths, one nibble per symbol (builds only)
-static_assert(kLens + 160 <= kSlice && kDecThreads * kSlice <= 163840, "LDS budget");
+constexpr int kRows = 80;          // dwords per lane (320 B)
+constexpr int kLitSorted = 0;      // bytes [0, 288): lit/len symbols in canonical order (low 8 bits)
+constexpr int kClTab = 0;          //   header only: bytes [0, 128): code-length-code table (u8: len<<5 | sym)
+constexpr int kLensLitRow = 32;    //   header only: rows 32..67: lit/len code lengths, 8 nibbles per row
+constexpr int kLensDistRow = 68;   //   header only: rows 68..71: distance code lengths
+constexpr int kDistSorted = 288;   // bytes [288, 320): distance symbols in canonical order
+constexpr int kEpoch = 4;          // iterations between input-window slides and token-chunk stores
 // A lane that reaches a block header parks; parked lanes build their tables together once kParkMin of the
-// wave's 64 lanes wait (or none is left decoding).  A table build is a serial loop of a few thousand
-// instructions per lane, so builds started one lane at a time would cost the whole wave 64× that.
+// wave's 64 lanes wait (or none is left decoding): a table build is a serial loop of a few thousand
+// instructions per lane, and builds started one lane at a time would cost the whole wave that much each.
 #ifndef SBAM_PARK_MIN
 #define SBAM_PARK_MIN 16
 #endif
@@ -54,11 +57,11 @@ constexpr int kParkMin = SBAM_PARK_MIN;
 
 constexpr uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-constexpr int kRing = 356;         // 128 B: per-lane input ring of 32 dwords (decode only; aliases kCnt/kLens)
-constexpr int kRingDw = 32;
-constexpr int kEpoch = 4;          // iterations between input-ring refills / token-chunk stores
-constexpr int kLoadDw = 16;        // dwords per ring refill (4 × 16-B loads)
-static_assert(kRing % 4 == 0 && kRing + 4 * kRingDw <= kSlice, "ring");
+struct Slice {  // one lane's interleaved LDS slice
+  uint8_t *base;
+  SB_DEV uint8_t *b(int i) const { return base + (i >> 2) * (kDecThreads * 4) + (i & 3); }
+  SB_DEV uint32_t *w(int row) const { return reinterpret_cast<uint32_t *>(base + row * (kDecThreads * 4)); }
+};
 
 // Compile-time loop: f(integral_constant<I>) for I in [B, E) — the index is a constant in the IR from the
 // start, so the per-length arrays below stay in registers (SROA) instead of a scratch array.
@@ -71,17 +74,18 @@ SB_DEV void sfor(F &&f) {
 }
 
 // Canonical code of one alphabet: lim[l] = left-justified (15-bit) end of the length-l codes; pk[l] =
-// (bse[l] << 5) | l with bse[l] = index of the first length-l symbol in canonical order minus its first code.
-// lim is non-decreasing in l, so the code length of the next 15 bits `rev` is 1 + #{l < 15 : rev >= lim[l]}
-// and one select per length (v_cmp + v_cndmask) finds pk of that length.
+// bse << 14 | hist << 5 | l, with bse = index (in canonical order) of the first length-l symbol minus its first
+// code, and hist = index of the first length-l symbol >= 256 (symbols of one length are in increasing order,
+// so the sorted table stores only their low 8 bits).  lim is non-decreasing in l, so the length of the code
+// in the next 15 bits `rev` is 1 + #{l < 15 : rev >= lim[l]}: one select per length finds its pk.
 struct Canon {
   uint32_t lim[16];
   int32_t pk[16];
 };
 
-// Decode the next symbol index: returns idx into the canonical symbol list (valid=false for an unassigned code,
-// which zlib reports after consuming 1 bit — the only incomplete codes it accepts are single 1-bit codes).
-SB_DEV int canon_decode(const Canon &c, uint64_t bb, int &len, bool &valid) {
+// Decode the next symbol index: idx into the canonical symbol list (valid=false for an unassigned code, which
+// zlib reports after consuming 1 bit — the only incomplete codes it accepts are single 1-bit codes).
+SB_DEV int canon_decode(const Canon &c, uint64_t bb, int &len, bool &valid, int &hist) {
   const uint32_t rev = __builtin_bitreverse32((uint32_t)bb) >> 17;
   int32_t p = c.pk[1];
   sfor<1, 15>([&](auto I) {
@@ -91,76 +95,98 @@ SB_DEV int canon_decode(const Canon &c, uint64_t bb, int &len, bool &valid) {
   const int L = p & 31;
   valid = rev < c.lim[15];
   len = valid ? L : 1;
-  return valid ? (int)(rev >> (15 - L)) + (p >> 5) : 0;
+  hist = (p >> 5) & 511;
+  return valid ? (int)(rev >> (15 - L)) + (p >> 14) : 0;
 }
 
-// Build the canonical structures of nsym code lengths (nibbles at LENS[sym0 ...]) into sorted (+hi bitmap).
-// Returns 0, or -1 for an over-subscribed set or an incomplete one other than a single 1-bit code
-// (zlib inflate_table).  A set with no codes at all is accepted (only possible for distances).
-SB_DEV int canon_build(uint8_t *sl, int sym0, int nsym, int sorted_off, bool lit, Canon &c) {
-  uint32_t *cnt = reinterpret_cast<uint32_t *>(sl + kCnt);
-  const uint32_t *lens = reinterpret_cast<const uint32_t *>(sl + kLens);
+// 15 counters of 9 bits (code lengths 1..15) in three u64: fields 0-6, 7-13, 14-15.
+struct Cnt15 {
+  uint64_t a = 0, b = 0, c = 0;
+  SB_DEV void add(uint32_t l, uint64_t v) {
+    const uint32_t w = (l >= 7) + (l >= 14);
+    const uint64_t inc = v << (9 * (l - 7 * w));
+    a += w == 0 ? inc : 0ull;
+    b += w == 1 ? inc : 0ull;
+    c += w == 2 ? inc : 0ull;
+  }
+  SB_DEV uint32_t get(uint32_t l) const {
+    const uint32_t w = (l >= 7) + (l >= 14);
+    const uint64_t x = w == 0 ? a : w == 1 ? b : c;
+    return (uint32_t)(x >> (9 * (l - 7 * w))) & 511u;
+  }
+};
+
+// Build the canonical structures of NW dwords of code-length nibbles (symbol s = nibble s) into the sorted
+// table at sorted_off.  Returns 0, or -1 for an over-subscribed set or an incomplete one other than a single
+// 1-bit code (zlib inflate_table).  A set with no codes at all is accepted (only possible for distances).
+template <int NW>
+SB_DEV int canon_build(const uint32_t (&lens)[NW], const Slice &sl, int sorted_off, bool lit, Canon &c) {
+  Cnt15 cnt, lo;
 #pragma unroll
-  for (int i = 0; i < 16; i++) cnt[i] = 0;
-  // count pass, 8 nibbles per step (the unused tail of a dword is masked off)
-  for (int s = 0; s < nsym; s += 8) {
-    const int n = sym0 + s;
-    const uint64_t two = (uint64_t)lens[n >> 3] | ((uint64_t)lens[(n >> 3) + 1] << 32);
-    uint32_t w = (uint32_t)(two >> (4 * (n & 7)));
-    if (nsym - s < 8) w &= (1u << (4 * (nsym - s))) - 1u;
-#pragma unroll
+  for (int dw = 0; dw < NW; dw++) {
+    const uint32_t w = lens[dw];
+#pragma unroll 1
     for (int j = 0; j < 8; j++) {
       const uint32_t v = (w >> (4 * j)) & 15u;
-      if (v) atomicAdd(&cnt[v], 1u);
+      if (v) {
+        cnt.add(v, 1);
+        if (lit && dw * 8 + j < 256) lo.add(v, 1);
+      }
     }
   }
   int left = 1, maxl = 0;
   bool over = false;
   uint32_t code = 0;
   int32_t offs = 0;
+  Cnt15 cur;
   sfor<1, 16>([&](auto I) {
     constexpr int l = decltype(I)::value;
-    const uint32_t k = cnt[l];
+    const uint32_t k = cnt.get(l);
     left = 2 * left - (int)k;
     over |= left < 0;
     maxl = k ? l : maxl;
     c.lim[l] = (code + k) << (15 - l);
-    c.pk[l] = (int32_t)(((uint32_t)(offs - (int32_t)code) << 5) | (uint32_t)l);
-    cnt[l] = (uint32_t)offs;  // fill cursor
+    const int32_t bse = offs - (int32_t)code;
+    const uint32_t hist = (uint32_t)offs + (lit ? lo.get(l) : 0u);
+    c.pk[l] = (int32_t)(((uint32_t)bse << 14) | (hist << 5) | (uint32_t)l);
+    cur.add(l, (uint64_t)offs);  // fill cursor
     offs += (int32_t)k;
     code = (code + k) << 1;
   });
   c.lim[0] = 0;
   c.pk[0] = 0;
   if (over || (left > 0 && maxl > 1)) return -1;
-  if (lit) {
-    uint32_t *hi = reinterpret_cast<uint32_t *>(sl + kLitHi);
 #pragma unroll
-    for (int i = 0; i < 9; i++) hi[i] = 0;
-  }
-  // fill pass: canonical order = by length, then by symbol (cursors advance in symbol order)
-  for (int s = 0; s < nsym; s += 8) {
-    const int n = sym0 + s;
-    const uint64_t two = (uint64_t)lens[n >> 3] | ((uint64_t)lens[(n >> 3) + 1] << 32);
-    uint32_t w = (uint32_t)(two >> (4 * (n & 7)));
-    if (nsym - s < 8) w &= (1u << (4 * (nsym - s))) - 1u;
-#pragma unroll
+  for (int dw = 0; dw < NW; dw++) {
+    const uint32_t w = lens[dw];
+#pragma unroll 1
     for (int j = 0; j < 8; j++) {
       const uint32_t v = (w >> (4 * j)) & 15u;
       if (v) {
-        const uint32_t pos = atomicAdd(&cnt[v], 1u);
-        sl[sorted_off + pos] = (uint8_t)(s + j);
-        if (lit && s + j >= 256)
-          atomicOr(reinterpret_cast<uint32_t *>(sl + kLitHi) + (pos >> 5), 1u << (pos & 31));
+        const uint32_t pos = cur.get(v);
+        cur.add(v, 1);
+        *sl.b(sorted_off + (int)pos) = (uint8_t)(dw * 8 + j);
       }
     }
   }
   return 0;
 }
 
+// A[i] for a lane-dependent i < 16: a 4-level tree of masked merges over registers (written as bit arithmetic:
+// a select tree is recognised as an indexed load and moved to scratch memory).
+SB_DEV uint32_t mrg(uint32_t a, uint32_t b, uint32_t m) { return a ^ ((a ^ b) & m); }
+SB_DEV uint32_t sel16(const uint32_t (&A)[16], uint32_t i) {
+  const uint32_t m0 = 0u - (i & 1u), m1 = 0u - ((i >> 1) & 1u), m2 = 0u - ((i >> 2) & 1u), m3 = 0u - ((i >> 3) & 1u);
+  uint32_t t[8], u[4];
+#pragma unroll
+  for (int k = 0; k < 8; k++) t[k] = mrg(A[2 * k], A[2 * k + 1], m0);
+#pragma unroll
+  for (int k = 0; k < 4; k++) u[k] = mrg(t[2 * k], t[2 * k + 1], m1);
+  return mrg(mrg(u[0], u[1], m2), mrg(u[2], u[3], m2), m3);
+}
+
 // Token output: an 8-slot shift register (t0 low half = oldest); a full chunk moves to the pending chunk p,
-// which leaves as one 16-B store at the next epoch (so stores and input loads issue together, and no
-// load wait in between covers a fresh store).
+// which leaves as one 16-B store at the next epoch (so stores issue together with the epoch's loads).
 struct TokOut {
   uint32_t t0, t1, t2, t3;
   uint32_t p0, p1, p2, p3;
@@ -219,28 +245,20 @@ __device__ unsigned long long g_dec_stats[16];
 #define DSTAT_ADD(slot, v) do {} while (0)
 #endif
 
-// Bit reader.  bb holds bc valid bits (LSB first); rp = block-relative index of the next payload dword to
-// enter bb; left = payload bits not yet consumed (negative ⇒ the symbol needed bits past the payload: zlib
-// returns for more input → SHORT).  While decoding symbols the dwords come from the lane's LDS ring
-// [rp, wp) (nx = ring[rp], read ahead); while parsing a block header they come straight from HBM.
+// Bit reader.  bb holds bc valid bits (LSB first); rp = block-relative index of the next payload dword to enter
+// bb; left = payload bits not yet consumed (negative ⇒ the symbol needed bits past the payload: zlib returns
+// for more input → SHORT).  While decoding symbols the dwords come from the lane's register window A (nx =
+// A[rp - ws], selected ahead); while parsing a block header they come straight from HBM.
 struct Bits {
   uint64_t bb;
   int bc;
   int left;
-  uint32_t rp, wp, nx;
+  uint32_t rp, nx;
   SB_DEV uint32_t peek(int n) const { return (uint32_t)bb & ((1u << n) - 1u); }
   SB_DEV void drop(int n) {
     bb >>= n;
     bc -= n;
     left -= n;
-  }
-  SB_DEV void refill_ring(const uint32_t *ring) {
-    if (bc <= 32) {
-      bb |= (uint64_t)nx << bc;
-      bc += 32;
-      rp++;
-      nx = ring[rp & (kRingDw - 1)];
-    }
   }
   SB_DEV void refill_hbm(const uint32_t *src) {
     if (bc <= 32) {
@@ -251,28 +269,30 @@ struct Bits {
   }
 };
 
-__global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t *__restrict__ d, int64_t D,
+__global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t *__restrict__ d, int64_t D,
                                                                    BlockTable bt, uint8_t *__restrict__ pool,
                                                                    uint32_t npages, unsigned int *pool_next,
                                                                    int32_t *__restrict__ blk_page,
                                                                    int32_t *__restrict__ status,
                                                                    int32_t *__restrict__ found,
                                                                    unsigned int *next_block) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_dec[kDecThreads * kSlice + 16];  // +16: 2-dword lens reads
-  uint8_t *sl = s_dec + threadIdx.x * kSlice;
-  const uint8_t *litS = sl + kLitSorted;
-  const uint32_t *litHi = reinterpret_cast<const uint32_t *>(sl + kLitHi);
-  const uint8_t *distS = sl + kDistSorted;
-  uint32_t *ring = reinterpret_cast<uint32_t *>(sl + kRing);
+  __shared__ __attribute__((aligned(16))) uint8_t s_dec[kRows * kDecThreads * 4];
+  const Slice sl{s_dec + 4 * threadIdx.x};
   const uint32_t *d32 = reinterpret_cast<const uint32_t *>(d);
 
   int state = S_NEXT;
   int64_t blk = -1;
   const uint32_t *src = d32;  // the block's payload, from its first (4-B aligned) dword
   uint32_t ldw = 0;           // payload dwords worth loading (payload + footer)
-  Bits br{0, 0, 0, 0, 0, 0};
-  uint32_t ld[kLoadDw];       // ring refill in flight (lands at the next epoch)
-  bool ldn = false;
+  Bits br{0, 0, 0, 0, 0};
+  // input window: A = payload dwords [ws, ws + 16), B = the next 8 (loaded one slide ahead); the window slides
+  // by 8 dwords at an epoch, so the compiler's wait for B always falls on a load issued epochs earlier
+  uint32_t A[16], B[8];
+  uint32_t ws = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) A[k] = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) B[k] = 0;
   TokOut to{0, 0, 0, 0, 0, 0, 0, 0, 0, false, 0};
   Canon lc, dc;
   int32_t o = 0, us = 0, err = INF_OK, sleft = 0, fin = 0;
@@ -281,6 +301,14 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
   uint64_t dt_ = __builtin_amdgcn_s_memtime();
   const uint64_t dt0_ = dt_;
 #endif
+  auto refill = [&]() {  // the symbol loop's refill: next dword from the register window
+    if (br.bc <= 32) {
+      br.bb |= (uint64_t)br.nx << br.bc;
+      br.bc += 32;
+      br.rp++;
+      br.nx = sel16(A, br.rp - ws);
+    }
+  };
 
   for (int it = 0;; it++) {
     if (state == S_NEXT) {
@@ -340,18 +368,21 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
     const bool any_hdr_ = __ballot(state == S_HDR) != 0;
 #endif
 
-    // --- epoch (wave-uniform): land the previous refill, store the pending token chunk, issue new refills.
-    // The loads issued here are first touched kEpoch iterations later, so the wait then is normally free.
+    // --- epoch (wave-uniform): slide the input window, store the pending token chunk, issue the next loads
     if ((it & (kEpoch - 1)) == 0) {
       const bool dec = state == S_HUFF || state == S_STORED;
-      if (ldn) {
-        if (dec) {
+      if (dec && br.rp - ws >= 8) {
 #pragma unroll
-          for (int j = 0; j < kLoadDw; j++) ring[(br.wp + j) & (kRingDw - 1)] = ld[j];
-          br.wp += kLoadDw;
-          br.nx = ring[br.rp & (kRingDw - 1)];
+        for (int k = 0; k < 8; k++) A[k] = A[k + 8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) A[k + 8] = B[k];
+        ws += 8;
+        if (ws + 16 < ldw) {
+          const uint4 *g = reinterpret_cast<const uint4 *>(src + ws + 16);
+          const uint4 x0 = g[0], x1 = g[1];
+          B[0] = x0.x; B[1] = x0.y; B[2] = x0.z; B[3] = x0.w;
+          B[4] = x1.x; B[5] = x1.y; B[6] = x1.z; B[7] = x1.w;
         }
-        ldn = false;  // a lane that left decoding drops its refill (its ring is rebuilt after the header)
       }
       if (to.pend && (dec || state == S_PARK || state == S_HDR)) {
         if (!tok_store(to, to.p0, to.p1, to.p2, to.p3, pool, pool_next, npages)) {
@@ -359,15 +390,6 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
           state = S_DONE;
         }
         to.pend = false;
-      }
-      if (dec && br.wp - br.rp <= (uint32_t)(kRingDw - kLoadDw) && br.wp < ldw) {
-        const uint4 *g = reinterpret_cast<const uint4 *>(src + br.wp);
-        const uint4 x0 = g[0], x1 = g[1], x2 = g[2], x3 = g[3];
-        ld[0] = x0.x; ld[1] = x0.y; ld[2] = x0.z; ld[3] = x0.w;
-        ld[4] = x1.x; ld[5] = x1.y; ld[6] = x1.z; ld[7] = x1.w;
-        ld[8] = x2.x; ld[9] = x2.y; ld[10] = x2.z; ld[11] = x2.w;
-        ld[12] = x3.x; ld[13] = x3.y; ld[14] = x3.z; ld[15] = x3.w;
-        ldn = true;
       }
     }
 
@@ -400,14 +422,14 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
             }
           }
         } else if (type == 1) {  // fixed codes: lit 0-143:8, 144-255:9, 256-279:7, 280-287:8; dist 0-31:5
-          uint32_t *lens = reinterpret_cast<uint32_t *>(sl + kLens);
-          for (int i = 0; i < 18; i++) lens[i] = 0x88888888u;        // 0..143
-          for (int i = 18; i < 32; i++) lens[i] = 0x99999999u;       // 144..255
-          for (int i = 32; i < 35; i++) lens[i] = 0x77777777u;       // 256..279
-          lens[35] = 0x88888888u;                                    // 280..287
-          for (int i = 36; i < 40; i++) lens[i] = 0x55555555u;       // 288..319: 32 distance codes
-          canon_build(sl, 0, 288, kLitSorted, true, lc);
-          canon_build(sl, 288, 32, kDistSorted, false, dc);
+          uint32_t llit[36], ldist[4];
+#pragma unroll
+          for (int i = 0; i < 36; i++)
+            llit[i] = i < 18 ? 0x88888888u : i < 32 ? 0x99999999u : i < 35 ? 0x77777777u : 0x88888888u;
+#pragma unroll
+          for (int i = 0; i < 4; i++) ldist[i] = 0x55555555u;
+          canon_build<4>(ldist, sl, kDistSorted, false, dc);
+          canon_build<36>(llit, sl, kLitSorted, true, lc);
           state = S_HUFF;
         } else if (type == 2) {  // dynamic codes
           br.refill_hbm(src);
@@ -461,24 +483,25 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
                 ok = 0;
               }
               if (ok == 1) {  // fill the 128-entry table: entries brev(code) + k·2^l
-                uint8_t *clt = sl + kClTab;
                 for (int s = 0; s < 19; s++) {
                   const int l = (int)((clp >> (3 * s)) & 7);
                   if (l) {
                     const uint32_t cv = (uint32_t)((next >> (8 * l)) & 0xff);
                     next += 1ull << (8 * l);
                     const uint32_t r = __builtin_bitreverse32(cv) >> (32 - l);
-                    for (uint32_t j = r; j < 128; j += 1u << l) clt[j] = (uint8_t)((l << 5) | s);
+                    for (uint32_t j = r; j < 128; j += 1u << l) *sl.b(kClTab + (int)j) = (uint8_t)((l << 5) | s);
                   }
                 }
-                // code lengths of hlit + hdist symbols (repeats may cross), one nibble each
-                uint32_t *lens = reinterpret_cast<uint32_t *>(sl + kLens);
+                // code lengths of hlit + hdist symbols (repeats may cross from the lit/len to the distance
+                // lengths), one nibble each: lit/len in rows kLensLitRow.., distance in rows kLensDistRow..
+#pragma unroll
+                for (int r = kLensLitRow; r < kLensDistRow + 4; r++) *sl.w(r) = 0;
                 const int total = hlit + hdist;
                 int n = 0;
                 uint32_t prev = 0, acc = 0;
                 while (n < total) {
                   br.refill_hbm(src);
-                  const uint32_t e = clt[br.peek(7)];
+                  const uint32_t e = *sl.b(kClTab + (int)br.peek(7));
                   const int l = (int)(e >> 5);
                   const uint32_t sym = e & 31;
                   if (br.left < l) { ok = -1; break; }
@@ -504,25 +527,33 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
                   }
                   if (n + rep > total) { ok = 0; break; }
                   const uint32_t pat = v * 0x11111111u;
-                  while (rep > 0) {  // up to the end of the current dword per step
-                    const int o8 = n & 7, k = min(rep, 8 - o8);
+                  while (rep > 0) {  // up to the end of the current dword (or of the lit/len lengths) per step
+                    const bool inlit = n < hlit;
+                    const int i = inlit ? n : n - hlit, end = inlit ? hlit : total;
+                    const int o8 = i & 7, k = min(rep, min(8 - o8, end - n));
                     const uint32_t m = (k == 8 ? 0xffffffffu : ((1u << (4 * k)) - 1u)) << (4 * o8);
                     acc |= pat & m;
                     n += k;
                     rep -= k;
-                    if ((n & 7) == 0) {
-                      lens[(n >> 3) - 1] = acc;
+                    if (((i + k) & 7) == 0 || n == end) {
+                      *sl.w((inlit ? kLensLitRow : kLensDistRow) + (i >> 3)) = acc;
                       acc = 0;
                     }
                   }
                   prev = v;
                 }
                 if (ok == 1) {
-                  if (n & 7) lens[n >> 3] = acc;
-                  if (((lens[32] & 15u) == 0)) ok = 0;  // invalid code -- missing end-of-block
+                  uint32_t llit[36], ldist[4];
+#pragma unroll
+                  for (int i = 0; i < 36; i++) llit[i] = *sl.w(kLensLitRow + i);
+#pragma unroll
+                  for (int i = 0; i < 4; i++) ldist[i] = *sl.w(kLensDistRow + i);
+                  if ((llit[32] & 15u) == 0) ok = 0;  // invalid code -- missing end-of-block
+                  // distance table first (its rows do not overlap the lengths); the lit/len table then
+                  // overwrites the lengths, which are in registers by now
+                  if (ok == 1 && canon_build<4>(ldist, sl, kDistSorted, false, dc) != 0) ok = 0;
+                  if (ok == 1 && canon_build<36>(llit, sl, kLitSorted, true, lc) != 0) ok = 0;
                 }
-                if (ok == 1 && canon_build(sl, 0, hlit, kLitSorted, true, lc) != 0) ok = 0;
-                if (ok == 1 && canon_build(sl, hlit, hdist, kDistSorted, false, dc) != 0) ok = 0;
               }
             }
             if (ok == 1) state = S_HUFF;
@@ -538,26 +569,25 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
         }
       }
       if (state == S_HUFF || state == S_STORED) {
-        // the tables overwrote the ring: prime it from HBM (one wait per header round)
-        const uint4 *g = reinterpret_cast<const uint4 *>(src + br.rp);
-        const uint4 x0 = g[0], x1 = g[1], x2 = g[2], x3 = g[3];
-        const uint32_t q = br.rp;
-        ring[(q + 0) & 31] = x0.x; ring[(q + 1) & 31] = x0.y; ring[(q + 2) & 31] = x0.z; ring[(q + 3) & 31] = x0.w;
-        ring[(q + 4) & 31] = x1.x; ring[(q + 5) & 31] = x1.y; ring[(q + 6) & 31] = x1.z; ring[(q + 7) & 31] = x1.w;
-        ring[(q + 8) & 31] = x2.x; ring[(q + 9) & 31] = x2.y; ring[(q + 10) & 31] = x2.z; ring[(q + 11) & 31] = x2.w;
-        ring[(q + 12) & 31] = x3.x; ring[(q + 13) & 31] = x3.y; ring[(q + 14) & 31] = x3.z; ring[(q + 15) & 31] = x3.w;
-        br.wp = q + 16;
-        br.nx = ring[q & 31];
-        ldn = false;  // a refill issued before the header is stale
+        // load the input window from HBM at the reader's position (one wait per header round)
+        ws = br.rp;
+        const uint4 *g = reinterpret_cast<const uint4 *>(src + ws);
+        const uint4 x0 = g[0], x1 = g[1], x2 = g[2], x3 = g[3], y0 = g[4], y1 = g[5];
+        A[0] = x0.x; A[1] = x0.y; A[2] = x0.z; A[3] = x0.w;
+        A[4] = x1.x; A[5] = x1.y; A[6] = x1.z; A[7] = x1.w;
+        A[8] = x2.x; A[9] = x2.y; A[10] = x2.z; A[11] = x2.w;
+        A[12] = x3.x; A[13] = x3.y; A[14] = x3.z; A[15] = x3.w;
+        B[0] = y0.x; B[1] = y0.y; B[2] = y0.z; B[3] = y0.w;
+        B[4] = y1.x; B[5] = y1.y; B[6] = y1.z; B[7] = y1.w;
+        br.nx = A[0];
       }
     } else if (state == S_HUFF) {
       // --- one literal/length symbol (+ its distance) per step
-      br.refill_ring(ring);
-      int L1;
+      refill();
+      int L1, h1;
       bool v1;
-      const int i1 = canon_decode(lc, br.bb, L1, v1);
-      const uint32_t hb = (litHi[i1 >> 5] >> (i1 & 31)) & 1u;
-      const int sym = (int)litS[i1] | (int)(hb << 8);
+      const int i1 = canon_decode(lc, br.bb, L1, v1, h1);
+      const int sym = (int)*sl.b(kLitSorted + i1) | (i1 >= h1 ? 256 : 0);
       if (br.left < L1) {
         err = INF_SHORT;
         state = S_DONE;
@@ -587,11 +617,11 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
           } else {
             const int len = lb + (int)br.peek(lx);
             br.drop(lx);
-            br.refill_ring(ring);
-            int L2;
+            refill();
+            int L2, h2;
             bool v2;
-            const int i2 = canon_decode(dc, br.bb, L2, v2);
-            const int ds = distS[i2];
+            const int i2 = canon_decode(dc, br.bb, L2, v2, h2);
+            const int ds = *sl.b(kDistSorted + i2);
             if (br.left < L2) {
               err = INF_SHORT;
               state = S_DONE;
@@ -627,7 +657,7 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
       }
     } else if (state == S_STORED) {
       // --- up to 2 stored bytes per step (byte-aligned: bb's low bits are the next byte)
-      br.refill_ring(ring);
+      refill();
       const int n = min(min(sleft, 2), us - o);
       int m = 0;
       for (int i = 0; i < 2; i++) {
@@ -668,7 +698,6 @@ __global__ __launch_bounds__(kDecThreads, 1) void k_inflate_decode(const uint8_t
       }
       to.n = 0;
       to.pend = false;
-      ldn = false;
       status[blk] = err;
       found[blk] = err == INF_OVERFLOW ? 0 : o;  // an overflowed block has no complete token stream
       state = S_NEXT;
