@@ -469,7 +469,7 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
     HIPCHK(c, ensure(&c->d_blkpage, &c->blkpage_cap, nb));
     if (!c->d_icnt) HIPCHK(c, dalloc(&c->d_icnt, 4));
     const int dec_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256 * 2);
-    const int res_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256 * 8);
+    const int res_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256 * 4);
     for (;;) {
       if (c->pool_cap < want) {
         dfree(c->d_pool);

@@ -172,17 +172,22 @@ SB_DEV int canon_build(const uint32_t (&lens)[NW], const Slice &sl, int sorted_o
   return 0;
 }
 
-// A[i] for a lane-dependent i < 16: a 4-level tree of masked merges over registers (written as bit arithmetic:
-// a select tree is recognised as an indexed load and moved to scratch memory).
-SB_DEV uint32_t mrg(uint32_t a, uint32_t b, uint32_t m) { return a ^ ((a ^ b) & m); }
+// A[i] for a lane-dependent i < 16: a 4-level tree of v_cndmask over registers, 4 compares + 15 selects.  The
+// selects are opaque asm: as plain selects the tree is recognised as an indexed load and moved to scratch memory.
+SB_DEV uint32_t csel(uint64_t m, uint32_t a, uint32_t b) {  // lane bit of m set ? b : a
+  uint32_t r;
+  asm("v_cndmask_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+  return r;
+}
 SB_DEV uint32_t sel16(const uint32_t (&A)[16], uint32_t i) {
-  const uint32_t m0 = 0u - (i & 1u), m1 = 0u - ((i >> 1) & 1u), m2 = 0u - ((i >> 2) & 1u), m3 = 0u - ((i >> 3) & 1u);
+  const uint64_t m0 = __builtin_amdgcn_ballot_w64((i & 1u) != 0), m1 = __builtin_amdgcn_ballot_w64((i & 2u) != 0),
+                 m2 = __builtin_amdgcn_ballot_w64((i & 4u) != 0), m3 = __builtin_amdgcn_ballot_w64((i & 8u) != 0);
   uint32_t t[8], u[4];
 #pragma unroll
-  for (int k = 0; k < 8; k++) t[k] = mrg(A[2 * k], A[2 * k + 1], m0);
+  for (int k = 0; k < 8; k++) t[k] = csel(m0, A[2 * k], A[2 * k + 1]);
 #pragma unroll
-  for (int k = 0; k < 4; k++) u[k] = mrg(t[2 * k], t[2 * k + 1], m1);
-  return mrg(mrg(u[0], u[1], m2), mrg(u[2], u[3], m2), m3);
+  for (int k = 0; k < 4; k++) u[k] = csel(m1, t[2 * k], t[2 * k + 1]);
+  return csel(m3, csel(m2, u[0], u[1]), csel(m2, u[2], u[3]));
 }
 
 // Token output: an 8-slot shift register (t0 low half = oldest); a full chunk moves to the pending chunk p,
@@ -712,28 +717,54 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
 }
 
 // ---- resolve kernel -------------------------------------------------------------------------------------------
+// One lane per BGZF block.  Both of its HBM streams are shaped for the memory side, which bounds this kernel:
+// with every block in flight, a lane's share of L2 is tens of bytes, so a 16-B access to a line costs the whole
+// line.  Tokens are read 64 B (32 tokens) at a time; output leaves in 64-B aligned groups of four 16-B stores
+// (the line is written whole while it is still in L2); a far copy is one unaligned 16-B load.
 constexpr int kResThreads = 256;
-constexpr int kResRing = 72;     // per-lane ring stride (64 B used): 18 dwords ⇒ ≤2-way bank conflicts, 8-B aligned
-constexpr int kNear = 40;     // copies with (effective) distance <= kNear read the ring
+constexpr int kResRing = 136;  // per-lane ring stride (128 B used): 34 dwords, 8-B aligned
+// Copies with (effective) distance <= kNear read the ring, longer ones HBM.  The flushed mark trails the output
+// by < 64 B when a copy starts, so a source 80 B back is stored; the ring still holds 105 B behind the output.
+constexpr int kNear = 80;
 
 struct TokIn {
-  uint32_t t0, t1, t2, t3;
-  int n;          // tokens left in t0..t3
-  uint64_t cur;   // byte offset of the next chunk in the pool
-  uint32_t pnext; // next page of this block
+  uint32_t t0, t1, t2, t3;  // current chunk (t0 low half = next token)
+  uint32_t q[12];           // up to three more chunks
+  int n;                    // tokens left in t0..t3
+  int nq;                   // chunks left in q
+  uint64_t cur;             // byte offset of the next 64-B group in the pool
+  uint32_t pnext;           // next page of this block
+  SB_DEV void load(const uint8_t *pool) {
+    const uint4 *g = reinterpret_cast<const uint4 *>(pool + cur);
+    const uint4 a = g[0], b = g[1], c = g[2], d = g[3];
+    if ((cur & (kTokPage - 1)) == 0) {  // a page's first group: chunk 0 links to the next page
+      pnext = a.x;
+      q[0] = b.x; q[1] = b.y; q[2] = b.z; q[3] = b.w;
+      q[4] = c.x; q[5] = c.y; q[6] = c.z; q[7] = c.w;
+      q[8] = d.x; q[9] = d.y; q[10] = d.z; q[11] = d.w;
+      t0 = t1 = t2 = t3 = 0;
+      nq = 3;
+    } else {
+      t0 = a.x; t1 = a.y; t2 = a.z; t3 = a.w;
+      q[0] = b.x; q[1] = b.y; q[2] = b.z; q[3] = b.w;
+      q[4] = c.x; q[5] = c.y; q[6] = c.z; q[7] = c.w;
+      q[8] = d.x; q[9] = d.y; q[10] = d.z; q[11] = d.w;
+      nq = 4;  // (t counts as the first)
+    }
+    cur += 64;
+    if ((cur & (kTokPage - 1)) == 0) cur = (uint64_t)pnext * kTokPage;
+  }
   SB_DEV uint32_t get(const uint8_t *pool) {
     if (n == 0) {
-      if ((cur & (kTokPage - 1)) == 0) {
-        pnext = *reinterpret_cast<const uint32_t *>(pool + cur);
-        cur += 16;
+      if (nq == 0) load(pool);
+      if (nq == 4) {
+        nq = 3;
+      } else {
+        t0 = q[0]; t1 = q[1]; t2 = q[2]; t3 = q[3];
+#pragma unroll
+        for (int k = 0; k < 8; k++) q[k] = q[k + 4];
+        nq--;
       }
-      const uint4 v = *reinterpret_cast<const uint4 *>(pool + cur);
-      t0 = v.x;
-      t1 = v.y;
-      t2 = v.z;
-      t3 = v.w;
-      cur += 16;
-      if ((cur & (kTokPage - 1)) == 0) cur = (uint64_t)pnext * kTokPage;
       n = 8;
     }
     const uint32_t t = t0 & 0xffffu;
@@ -746,7 +777,7 @@ struct TokIn {
   }
 };
 
-__global__ __launch_bounds__(kResThreads, 8) void k_inflate_resolve(BlockTable bt, uint8_t *__restrict__ out,
+__global__ __launch_bounds__(kResThreads, 4) void k_inflate_resolve(BlockTable bt, uint8_t *__restrict__ out,
                                                                     const uint8_t *__restrict__ pool,
                                                                     const int32_t *__restrict__ blk_page,
                                                                     const int32_t *__restrict__ found,
@@ -754,14 +785,24 @@ __global__ __launch_bounds__(kResThreads, 8) void k_inflate_resolve(BlockTable b
   __shared__ __attribute__((aligned(16))) uint8_t s_ring[kResThreads * kResRing];
   uint8_t *ring = s_ring + threadIdx.x * kResRing;
   uint32_t *ring32 = reinterpret_cast<uint32_t *>(ring);
-  const uint32_t *out32 = reinterpret_cast<const uint32_t *>(out);
 
   // positions are byte offsets into `out` (kept as offsets so every access stays a global, not flat, access;
   // `out` is 256-B aligned, so offset alignment is address alignment)
   bool active = false, exited = false;
   int64_t a = 0, ae = 0, fl = 0;
-  TokIn ti{0, 0, 0, 0, 0, 0, 0};
+  TokIn ti;
+  ti.t0 = ti.t1 = ti.t2 = ti.t3 = 0;
+#pragma unroll
+  for (int k = 0; k < 12; k++) ti.q[k] = 0;
+  ti.n = ti.nq = 0;
+  ti.cur = 0;
+  ti.pnext = 0;
   int crem = 0, eff = 0, npad = 0;
+  auto flush16 = [&](int64_t x) {  // the aligned 16-B chunk at x (ring stride is 8-B aligned)
+    const uint2 lo = *reinterpret_cast<const uint2 *>(ring + (x & 127));
+    const uint2 hi = *reinterpret_cast<const uint2 *>(ring + ((x + 8) & 127));
+    *reinterpret_cast<uint4 *>(out + x) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+  };
 
   for (;;) {
     if (!active && !exited) {
@@ -775,7 +816,7 @@ __global__ __launch_bounds__(kResThreads, 8) void k_inflate_resolve(BlockTable b
           a = bt.uoff[b];
           ae = a + f;
           fl = a;
-          ti.n = 0;
+          ti.n = ti.nq = 0;
           ti.cur = (uint64_t)pg * kTokPage;
           crem = 0;
           npad = 0;
@@ -789,7 +830,7 @@ __global__ __launch_bounds__(kResThreads, 8) void k_inflate_resolve(BlockTable b
     if (crem == 0) {
       const uint32_t t = ti.get(pool);
       if (t < 256) {
-        ring[a & 63] = (uint8_t)t;
+        ring[a & 127] = (uint8_t)t;
         a++;
       } else if (t != kTokPad) {
         crem = (int)t - 253;
@@ -802,58 +843,74 @@ __global__ __launch_bounds__(kResThreads, 8) void k_inflate_resolve(BlockTable b
       const int n = min(min(crem, 16), min(eff, (int)(ae - a)));
       const int64_t src = a - eff;
       uint32_t v0, v1, v2, v3;
-      const int sh = (int)(src & 3);
       if (eff <= kNear) {  // source in the ring: 5 dwords around it
-        const int q = (int)((src & 63) >> 2);
-        const uint32_t s0 = ring32[q & 15], s1 = ring32[(q + 1) & 15], s2 = ring32[(q + 2) & 15],
-                       s3 = ring32[(q + 3) & 15], s4 = ring32[(q + 4) & 15];
+        const int sh = (int)(src & 3);
+        const int q = (int)((src & 127) >> 2);
+        const uint32_t s0 = ring32[q & 31], s1 = ring32[(q + 1) & 31], s2 = ring32[(q + 2) & 31],
+                       s3 = ring32[(q + 3) & 31], s4 = ring32[(q + 4) & 31];
         v0 = __builtin_amdgcn_alignbyte(s1, s0, sh);
         v1 = __builtin_amdgcn_alignbyte(s2, s1, sh);
         v2 = __builtin_amdgcn_alignbyte(s3, s2, sh);
         v3 = __builtin_amdgcn_alignbyte(s4, s3, sh);
-      } else {  // source already stored to HBM (it lies below the flushed mark)
-        const uint32_t *g = out32 + (src >> 2);
-        const uint4 x = *reinterpret_cast<const uint4 *>(g);
-        const uint32_t x4 = g[4];
-        v0 = __builtin_amdgcn_alignbyte(x.y, x.x, sh);
-        v1 = __builtin_amdgcn_alignbyte(x.z, x.y, sh);
-        v2 = __builtin_amdgcn_alignbyte(x.w, x.z, sh);
-        v3 = __builtin_amdgcn_alignbyte(x4, x.w, sh);
+      } else {  // source already stored to HBM (it lies below the flushed mark): one unaligned 16-B load
+        const uint4 x = *reinterpret_cast<const uint4 *>(out + src);
+        v0 = x.x;
+        v1 = x.y;
+        v2 = x.z;
+        v3 = x.w;
       }
       // write 16 bytes at a (bytes past a + n are scratch, rewritten before they are flushed):
       // head bytes up to the next dword boundary, then 4 aligned dwords
       const int h = (int)((4 - (a & 3)) & 3);
 #pragma unroll
       for (int k = 0; k < 3; k++)
-        if (k < h) ring[(a + k) & 63] = (uint8_t)(v0 >> (8 * k));
+        if (k < h) ring[(a + k) & 127] = (uint8_t)(v0 >> (8 * k));
       const uint32_t w0 = __builtin_amdgcn_alignbyte(v1, v0, h), w1 = __builtin_amdgcn_alignbyte(v2, v1, h),
                      w2 = __builtin_amdgcn_alignbyte(v3, v2, h), w3 = __builtin_amdgcn_alignbyte(0u, v3, h);
-      const int q = (int)(((a + h) & 63) >> 2);
-      ring32[q & 15] = w0;
-      ring32[(q + 1) & 15] = w1;
-      ring32[(q + 2) & 15] = w2;
-      ring32[(q + 3) & 15] = w3;
+      const int q = (int)(((a + h) & 127) >> 2);
+      ring32[q & 31] = w0;
+      ring32[(q + 1) & 31] = w1;
+      ring32[(q + 2) & 31] = w2;
+      ring32[(q + 3) & 31] = w3;
       a += n;
       crem -= n;
       if (n == eff && eff < 16) eff *= 2;  // the copied bytes extend the period: distance 2·eff is valid
     }
-    // flush: a block's partial first chunk (shared with the previous block) as bytes, then aligned 16-B chunks
+    // flush: a block's partial first chunk (shared with the previous block) as bytes, then aligned 16-B
+    // chunks up to a 64-B boundary, then whole 64-B groups
     if (fl & 15) {
       const int64_t hd = (fl & ~(int64_t)15) + 16;
       if (a >= hd || a == ae) {
         const int64_t lim = a < hd ? a : hd;
-        for (int64_t x = fl; x < lim; x++) out[x] = ring[x & 63];
+        for (int64_t x = fl; x < lim; x++) out[x] = ring[x & 127];
         fl = lim;
       }
     }
-    while ((fl & 15) == 0 && a - fl >= 16) {
-      const uint2 lo = *reinterpret_cast<const uint2 *>(ring + (fl & 63));
-      const uint2 hi = *reinterpret_cast<const uint2 *>(ring + ((fl + 8) & 63));
-      *reinterpret_cast<uint4 *>(out + fl) = make_uint4(lo.x, lo.y, hi.x, hi.y);
-      fl += 16;
+    if ((fl & 15) == 0) {
+      if ((fl & 63) == 0) {
+        if (a - fl >= 64) {
+          const uint2 *r = reinterpret_cast<const uint2 *>(ring + (fl & 127));
+          const uint2 x0 = r[0], x1 = r[1], x2 = r[2], x3 = r[3], x4 = r[4], x5 = r[5], x6 = r[6], x7 = r[7];
+          uint4 *o = reinterpret_cast<uint4 *>(out + fl);
+          o[0] = make_uint4(x0.x, x0.y, x1.x, x1.y);
+          o[1] = make_uint4(x2.x, x2.y, x3.x, x3.y);
+          o[2] = make_uint4(x4.x, x4.y, x5.x, x5.y);
+          o[3] = make_uint4(x6.x, x6.y, x7.x, x7.y);
+          fl += 64;
+        }
+      } else {
+        while ((fl & 63) != 0 && a - fl >= 16) {
+          flush16(fl);
+          fl += 16;
+        }
+      }
     }
-    if (a == ae) {  // tail (shared with the next block) as bytes
-      for (int64_t x = fl; x < ae; x++) out[x] = ring[x & 63];
+    if (a == ae) {  // tail (shared with the next block): whole 16-B chunks, then bytes
+      while (ae - fl >= 16) {
+        flush16(fl);
+        fl += 16;
+      }
+      for (int64_t x = fl; x < ae; x++) out[x] = ring[x & 127];
       fl = ae;
       active = false;
     }
