@@ -40,6 +40,25 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def measured_traffic(kernel: str, args):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes (tools/traffic_pmc.py →
+    profiles/*/traffic.json), when they were taken on this same workload; else None.  FETCH_SIZE is doubled
+    for the kernels' 16-B/lane streaming reads (MI355X_MICROARCH.md, HBM/rocprofv3: gfx950 tallies each
+    128-B request at 64 B); WRITE_SIZE is used as reported."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json")), reverse=True):
+        try:
+            t = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if t.get("workload") != {"size_gb": args.size_gb, "seed": args.seed, "tile_mb": args.tile_mb}:
+            continue
+        k = t.get("kernels", {}).get(kernel)
+        if k:
+            return {"hbm_bytes_per_launch": k["hbm_bytes_per_launch"], "source": os.path.relpath(path, ROOT)}
+    return None
+
+
 def cpu_baseline(sample_mb: float, threads: int, split_size: int, seed: int):
     """Oracle (C restatement of the reference algorithm) on a bounded sample of the same synthetic stream:
     zlib inflate + full checker at every position + compute-splits, `threads` host threads."""
@@ -116,13 +135,15 @@ def main():
     res = None
     for _ in range(args.warmup):
         res = step()
-    kernels = ("scan", "chain", "inflate", "inflate_decode", "inflate_resolve", "check_full", "find_record",
-               "records")
+    kernels = ("scan", "chain", "inflate", "inflate_decode", "inflate_resolve", "check_full", "check_pass0",
+               "check_chains", "find_record", "records")
     tot_ms = {k: 0.0 for k in kernels}
     sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        ts = time.perf_counter()
         res = step()
+        log(f"[rank {rank}] step {i}: {(time.perf_counter() - ts) * 1e3:.1f} ms (host wall)")
         for k in kernels:
             ms = shard.f.kernel_ms(k)
             tot_ms[k] += max(ms, 0.0)
@@ -149,16 +170,18 @@ def main():
     if not parity["ok"]:
         log(f"[rank {rank}] PARITY PROPERTY FAILED: {parity}")
 
-    # --- roofline of the dominant kernel (this rank's shard; per launch)
+    # --- roofline of the dominant kernel (this rank's shard; per launch).  Candidates are single kernels:
+    # k_check<0> (record-0 pass: reads U, writes the U/8 PASS0 bitmap), k_inflate_decode (reads the C payload;
+    # its token stream is an internal intermediate) and k_inflate_resolve (writes U; tokens internal).
     st, cs, us, uo = f.blocks()
     comp_payload = int(cs.astype(np.int64).sum())
     U = int(f.uncompressed_size)
     avg = {k: tot_ms[k] / args.steps for k in kernels}
-    alg = {"inflate": comp_payload + U, "check_full": U + U // 8,
-           "scan": 2 * int(f._buf.size), "records": 0, "find_record": 0, "chain": 0, "inflate_decode": 0,
-           "inflate_resolve": 0}
-    dom = max(("inflate", "check_full", "scan"), key=lambda k: avg[k])
+    alg = {"check_pass0": U + U // 8, "inflate_decode": comp_payload, "inflate_resolve": U}
+    names = {"check_pass0": "k_check<0>", "inflate_decode": "k_inflate_decode", "inflate_resolve": "k_inflate_resolve"}
+    dom = max(alg, key=lambda k: avg[k])
     achieved = alg[dom] / (avg[dom] * 1e-3) / 1e9 if avg[dom] > 0 else 0.0
+    traffic = measured_traffic(names[dom], args)
 
     if rank == 0:
         cpu = None
@@ -188,13 +211,13 @@ def main():
                        "parallelism": f"shard{world}"},
             "uncompressed_gbps": round(U * world * args.steps / elapsed / 1e9, 3),
             "kernel_ms": {k: round(v, 3) for k, v in avg.items()},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "algorithmic_bytes": alg[dom]},
-            "checker_roofline": {"achieved": round(alg["check_full"] / (avg["check_full"] * 1e-3) / 1e9, 2)
-                                 if avg["check_full"] > 0 else None,
-                                 "frac": round(alg["check_full"] / (avg["check_full"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                                 if avg["check_full"] > 0 else None},
+            "roofline": {"bound": "hbm", "kernel": names[dom], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic["hbm_bytes_per_launch"] if traffic else None,
+                         "traffic_source": traffic["source"] if traffic else None,
+                         "algorithmic_bytes": alg[dom], "avg_launch_ms": round(avg[dom], 3)},
+            "stage_rooflines": {k: {"achieved": round(alg[k] / (avg[k] * 1e-3) / 1e9, 2) if avg[k] > 0 else None,
+                                    "algorithmic_bytes": alg[k], "avg_launch_ms": round(avg[k], 3)} for k in alg},
             "cpu_baseline": cpu,
             "parity": parity,
         }

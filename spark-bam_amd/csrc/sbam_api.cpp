@@ -682,7 +682,12 @@ int sbam_check_full_counts(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, int32
   cd.totals = cd.scalars + 4;
   {
     Timer t(c, "check_full");
-    HIPCHK(c, launch_check_full_counts(view(c), x0, x1, R, by_key, cd, c->d_bitmap, c->stream));
+    {
+      Timer t0(c, "check_pass0");
+      HIPCHK(c, launch_check_full_counts(view(c), x0, x1, R, by_key, cd, c->d_bitmap, c->stream));
+    }
+    Timer t1(c, "check_chains");
+    HIPCHK(c, launch_check_full_chains(view(c), x0, x1, R, by_key, cd, c->d_bitmap, c->stream));
   }
   std::vector<unsigned long long> h(kCountsWords);
   HIPCHK(c, hipMemcpyAsync(h.data(), c->d_counts, kCountsWords * 8, hipMemcpyDeviceToHost, c->stream));

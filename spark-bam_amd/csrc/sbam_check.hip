@@ -762,6 +762,11 @@ hipError_t launch_check_full_counts(StreamView sv, int64_t x0, int64_t x1, int32
     hipLaunchKernelGGL(k_check<MODE_BYKEY>, dim3(g), dim3(kCheckThreads), 0, s, sv, x0, x1, R, cd, bitmap, nullptr);
   else
     hipLaunchKernelGGL(k_check<MODE_COUNTS>, dim3(g), dim3(kCheckThreads), 0, s, sv, x0, x1, R, cd, bitmap, nullptr);
+  return hipGetLastError();
+}
+hipError_t launch_check_full_chains(StreamView sv, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,
+                                    unsigned long long *bitmap, hipStream_t s) {
+  if (x1 <= x0) return hipSuccess;
   hipLaunchKernelGGL(k_chains, dim3(chain_grid(x0, x1)), dim3(256), 0, s, sv, x0, x1, R, bitmap, cd, by_key, nullptr);
   return hipGetLastError();
 }

@@ -78,6 +78,9 @@ hipError_t launch_lower_bound(const Candidate *c, int64_t n, int64_t q, int64_t 
 // Bitmaps cover [x0 & ~63, x1): bit (x - (x0 & ~63)) = call at x (0 for x < x0).
 hipError_t launch_check_full_counts(StreamView sv, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,
                                     unsigned long long *bitmap, hipStream_t s);
+// (launch_check_full_counts runs the record-0 pass; launch_check_full_chains then resolves the PASS0 chains)
+hipError_t launch_check_full_chains(StreamView sv, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,
+                                    unsigned long long *bitmap, hipStream_t s);
 hipError_t launch_check_eager(StreamView sv, int64_t x0, int64_t x1, int32_t R, unsigned long long *bitmap,
                               hipStream_t s);
 hipError_t launch_check_words(StreamView sv, int64_t x0, int64_t x1, int32_t R, uint32_t *words,

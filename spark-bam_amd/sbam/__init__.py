@@ -423,15 +423,25 @@ class BamFile:
                       bgzf_blocks_to_check: int = BGZF_BLOCKS_TO_CHECK, reads_to_check: int = READS_TO_CHECK,
                       max_read_size: int = MAX_READ_SIZE, use_success_bitmap: bool = False):
         """Per Hadoop split: (first record Pos, non-empty?, record count)."""
+        bp, off, nonempty, n = self.split_records_arrays(split_size, first, count, bgzf_blocks_to_check,
+                                                         reads_to_check, max_read_size, use_success_bitmap)
+        return [(Pos(int(bp[i]), int(off[i])), bool(nonempty[i]), int(n[i])) for i in range(bp.size)]
+
+    def split_records_arrays(self, split_size: int, first: int = 0, count: Optional[int] = None,
+                             bgzf_blocks_to_check: int = BGZF_BLOCKS_TO_CHECK, reads_to_check: int = READS_TO_CHECK,
+                             max_read_size: int = MAX_READ_SIZE, use_success_bitmap: bool = False):
+        """split_records as arrays (first record block_pos, offset, non-empty, record count): no per-split
+        Python objects (a 10 GB file has ~5000 splits)."""
         ns = len(hadoop_splits(self.file_size, split_size))
         count = ns - first if count is None else count
-        fp = (_Pos * max(count, 1))()
+        fp = np.zeros(max(count, 1), dtype=[("block_pos", "<i8"), ("offset", "<i4"), ("reserved", "<i4")])
         fd = np.zeros(max(count, 1), np.int32)
         nr = np.zeros(max(count, 1), np.int64)
         a = self._args(split_size, bgzf_blocks_to_check, reads_to_check, max_read_size, use_success_bitmap)
-        self._check(self.L.sbam_split_records(self.ctx, ctypes.byref(a), first, count, ctypes.addressof(fp),
+        self._check(self.L.sbam_split_records(self.ctx, ctypes.byref(a), first, count, fp.ctypes.data,
                                               _ptr(fd), _ptr(nr)))
-        return [(_pos(fp[i]), bool(fd[i]), int(nr[i])) for i in range(count)]
+        return (fp["block_pos"][:count].copy(), fp["offset"][:count].astype(np.int64), fd[:count] != 0,
+                nr[:count].copy())
 
     def partition_sizes(self, split_size: int, **kw) -> List[int]:
         """records.partitionSizes of sc.loadReads / loadBam (LoadBAMTest.scala:24-45)."""

@@ -91,21 +91,21 @@ def shard_pass(f, p: ShardPlan, split_size: int, R: int = 10) -> ShardResult:
     """One shard's hot path once its stream is inflated (``f``: sbam.BamFile over the shard's bytes, or any
     object with the same methods): full check of the positions of the blocks the shard owns (from its first
     block to the block where the next shard starts), then the owned Hadoop splits' first records and counts."""
-    st, _, _, uo = f.blocks()
     if p.owned_hi >= p.file_size:
         x1 = f.uncompressed_size
     else:
+        st, _, _, uo = f.blocks()
         nb = f.find_block_start(p.owned_hi)
         b = int(np.searchsorted(st, nb))
         x1 = int(uo[b]) if b < st.size else f.uncompressed_size
     counts = f.check_full_counts(0, x1, R)
-    recs = f.split_records(split_size, first=p.split_first, count=p.split_count, reads_to_check=R,
-                           use_success_bitmap=True) if p.split_count else []
-    return ShardResult(pack_counts(counts),
-                       np.array([r[0].block_pos for r in recs], np.int64),
-                       np.array([r[0].offset for r in recs], np.int64),
-                       np.array([int(r[1]) for r in recs], np.int64),
-                       np.array([r[2] for r in recs], np.int64))
+    if p.split_count:
+        bp, off, nonempty, n = f.split_records_arrays(split_size, first=p.split_first, count=p.split_count,
+                                                      reads_to_check=R, use_success_bitmap=True)
+    else:
+        bp = off = nonempty = n = np.zeros(0, np.int64)
+    return ShardResult(pack_counts(counts), bp.astype(np.int64), off.astype(np.int64), nonempty.astype(np.int64),
+                       n.astype(np.int64))
 
 
 class GpuShard:

@@ -46,6 +46,11 @@ class OracleShard:
             out.append((sbam.Pos(p.block_pos, p.offset), len(chain) > 0, len(chain)))
         return out
 
+    def split_records_arrays(self, split_size, first, count, reads_to_check, use_success_bitmap):
+        recs = self.split_records(split_size, first, count, reads_to_check, use_success_bitmap)
+        return (np.array([r[0].block_pos for r in recs], np.int64), np.array([r[0].offset for r in recs], np.int64),
+                np.array([r[1] for r in recs], bool), np.array([r[2] for r in recs], np.int64))
+
 
 def _worker(rank, world, port, name, split_size, q):
     import torch.distributed as dist

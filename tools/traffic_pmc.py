@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of the hot kernels from rocprofv3 --pmc passes (one counter group per pass, as the
+MI355X guide prescribes: FETCH_SIZE and WRITE_SIZE cannot share a pass).
+
+    traffic_pmc.py OUT.json FETCH_DIR WRITE_DIR [--size-gb G] [--seed S] [--tile-mb T]
+
+FETCH_DIR / WRITE_DIR hold p_counter_collection.csv of a `--pmc FETCH_SIZE` and a `--pmc WRITE_SIZE` run of
+tools/bench_kernels.py on the bench workload.  Values are KB per dispatch; per kernel the median dispatch is
+kept.  Corrections (MI355X_MICROARCH.md, HBM/rocprofv3 section): FETCH_SIZE is doubled — gfx950 tallies each
+128-B request at 64 B for 16-B/lane reads, which is how every one of these kernels reads; WRITE_SIZE is exact
+for 16-B/lane stores and is used as reported.  FETCH counts Infinity-Cache hits too (memory-side requests)."""
+import argparse
+import csv
+import json
+import os
+import statistics
+from collections import defaultdict
+
+KERNELS = {"k_check<0>": "sbam::k_check<0>", "k_chains": "sbam::k_chains",
+           "k_inflate_decode": "sbam::k_inflate_decode", "k_inflate_resolve": "sbam::k_inflate_resolve",
+           "k_scan_count": "sbam::k_scan_count", "k_scan_write": "sbam::k_scan_write",
+           "k_record_counts": "sbam::k_record_counts"}
+
+
+def per_dispatch(d, counter):
+    vals = defaultdict(list)
+    for r in csv.DictReader(open(os.path.join(d, "p_counter_collection.csv"))):
+        if r["Counter_Name"] != counter:
+            continue
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        for k, prefix in KERNELS.items():
+            if name == prefix:
+                vals[k].append(float(r["Counter_Value"]) * 1024.0)  # KB → bytes
+    return {k: statistics.median(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out")
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("--size-gb", type=float, default=10.0)
+    ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EEDBA11)
+    ap.add_argument("--tile-mb", type=float, default=64.0)
+    a = ap.parse_args()
+    fetch, nf = per_dispatch(a.fetch_dir, "FETCH_SIZE")
+    write, nw = per_dispatch(a.write_dir, "WRITE_SIZE")
+    out = {"workload": {"size_gb": a.size_gb, "seed": a.seed, "tile_mb": a.tile_mb},
+           "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes of tools/bench_kernels.py; "
+                     "median dispatch; FETCH x2 (gfx950 64-B tally of 128-B requests), WRITE as reported",
+           "kernels": {}}
+    for k in sorted(set(fetch) & set(write)):
+        f2 = 2.0 * fetch[k]
+        out["kernels"][k] = {"fetch_size_reported": fetch[k], "fetch_bytes": f2, "write_bytes": write[k],
+                             "hbm_bytes_per_launch": int(f2 + write[k]), "dispatches": [nf[k], nw[k]]}
+    json.dump(out, open(a.out, "w"), indent=1)
+    print(json.dumps(out["kernels"]))
+
+
+if __name__ == "__main__":
+    main()
