@@ -15,6 +15,8 @@
 // time (SWAR).  Positions whose first record passes (true starts and rare near-misses) continue the
 // 10-record chain from global memory.  Counts are accumulated per lane in carry-save bit planes (19 flags)
 // and packed 8-bit key counters, reduced with ballots once per 7 tiles.
+#include <type_traits>
+
 #include "sbam_internal.h"
 
 #ifndef SBAM_ABLATE
@@ -286,11 +288,12 @@ struct Tile {
   int64_t base;
 };
 
+// 64 bits of an LDS bitmap from bit x: two funnel shifts (v_alignbit), no branch on the bit offset
 SB_DEV uint64_t bits64(const uint32_t *bm, int x) {
-  const int w = x >> 5, s = x & 31;
-  const uint64_t lo = (uint64_t)bm[w] | ((uint64_t)bm[w + 1] << 32);
-  const uint64_t hi = bm[w + 2];
-  return s ? (lo >> s) | (hi << (64 - s)) : lo;
+  const int w = x >> 5;
+  const uint32_t s = (uint32_t)x & 31u;
+  const uint32_t a = bm[w], b = bm[w + 1], c = bm[w + 2];
+  return ((uint64_t)__builtin_amdgcn_alignbit(c, b, s) << 32) | __builtin_amdgcn_alignbit(b, a, s);
 }
 
 // Any byte of the name body [rel, rel + n) outside allowedReadNameChars? (n <= 254, inside the window)
@@ -328,8 +331,11 @@ SB_DEV uint32_t ref_bits_lds(int32_t ri, int32_t rp, const int32_t *lensL, int32
 // Record 0 at x (full.Checker.scala:22-184 / eager.Checker.scala:24-126 for k = 0), fixed fields in f[],
 // rel = x - tile base.  Every check is evaluated unconditionally from the tile (clamped LDS reads, no
 // per-lane branches) so a wave's lanes cost the same; only the rare tails (a name body or an op array
-// running past 64 checked bytes / ops) branch out to HBM.
-template <bool EAGER>
+// running past 64 checked bytes / ops) branch out to HBM.  INTERIOR: the tile ends at least kInteriorTail
+// bytes before the stream end, so no read of record 0 (36 fixed bytes, <= 255 name bytes, <= 65535 ops) can
+// reach EOF and the EOF arithmetic drops out.
+constexpr int64_t kInteriorTail = 262144 + 512;
+template <bool EAGER, bool INTERIOR>
 SB_DEV uint32_t check_first(const Tile &t, const StreamView &sv, const int32_t *lensL, int64_t x, int rel, int R,
                             const int32_t f[8]) {
   if (R == 0) return W_PASS0;  // Success(0): resolved by the chain pass
@@ -341,11 +347,11 @@ SB_DEV uint32_t check_first(const Tile &t, const StreamView &sv, const int32_t *
   const uint32_t rb1 = lensL ? ref_bits_lds(nri, nrp, lensL, sv.nref) : ref_err(nri, nrp, nullptr, sv.lens, sv.nref);
   const uint32_t Fref = (rb0 << 1) | (rb1 << 5) | (too_few_remaining(bs, lrn, nc, ls) ? (1u << 18) : 0u);
   const bool empty_mapped = (flag & 4u) == 0 && (ls == 0 || nc == 0);
-  if (EAGER && x + 36 <= sv.L && (Fref || lrn < 2 || empty_mapped))
+  if (EAGER && (INTERIOR || x + 36 <= sv.L) && (Fref || lrn < 2 || empty_mapped))
     return Fref ? Fref : (1u << 12);  // eager: ~96 % of positions end here, skip the rest of the record
   // read name: lrn 0/1 → noReadName / emptyReadName (name not consumed); else last byte NUL, then characters
   const bool has_name = lrn >= 2;
-  const bool name_eof = has_name && x + 36 + lrn > sv.L;
+  const bool name_eof = !INTERIOR && has_name && x + 36 + lrn > sv.L;
   const uint32_t last = t.win[rel + 35 + (has_name ? lrn : 1)];
   const bool nonnull = has_name && last != 0;
   const bool scan = has_name && last == 0;
@@ -358,14 +364,17 @@ SB_DEV uint32_t check_first(const Tile &t, const StreamView &sv, const int32_t *
   const int32_t clen = has_name ? lrn : 0;
   const int64_t c = x + 36 + clen;
   const int crel = rel + 36 + clen;
-  const int64_t n_eof64 = (sv.L - c) >> 2;
-  const int32_t n_eof = n_eof64 < 0 ? 0 : n_eof64 > 0x7fffffff ? 0x7fffffff : (int32_t)n_eof64;
+  int32_t n_eof = 0x7fffffff;
+  if (!INTERIOR) {
+    const int64_t n_eof64 = (sv.L - c) >> 2;
+    n_eof = n_eof64 < 0 ? 0 : n_eof64 > 0x7fffffff ? 0x7fffffff : (int32_t)n_eof64;
+  }
   const int32_t lim = n_eof < nc ? n_eof : nc;
   const uint64_t om = bits64(t.opc + (crel & 3) * kOpcWords, crel >> 2);
   int32_t bad = om ? (int32_t)__builtin_ctzll(om) : 64;
   if (om == 0 && lim > 64 && !name_eof) bad = first_bad_op(t, sv, c, lim);
   const bool inv_op = nc > 0 && bad < lim;
-  const bool few_ops = nc > 0 && !inv_op && n_eof < nc;
+  const bool few_ops = !INTERIOR && nc > 0 && !inv_op && n_eof < nc;
   uint32_t F = Fref;
   F |= lrn == 0 ? (1u << 12) : 0u;
   F |= lrn == 1 ? (1u << 13) : 0u;
@@ -375,7 +384,7 @@ SB_DEV uint32_t check_first(const Tile &t, const StreamView &sv, const int32_t *
   F |= few_ops ? (1u << 14) : 0u;
   F |= (empty_mapped && !inv_op && !few_ops) ? (((ls == 0) ? (1u << 16) : 0u) | ((nc == 0) ? (1u << 17) : 0u)) : 0u;
   // result, in the reference's order of early exits
-  const bool fixed_eof = x + 36 > sv.L;
+  const bool fixed_eof = !INTERIOR && x + 36 > sv.L;
   uint32_t w;
   if (EAGER) {  // eager.Checker: false at the first failing group (only pass/fail and HALO matter)
     const bool fail_fixed = Fref || !has_name || empty_mapped;
@@ -512,7 +521,7 @@ SB_DEV void bykey_count(uint32_t *s_cnt, int lane, bool counted, uint32_t key, u
 }
 
 template <int MODE>
-__global__ __launch_bounds__(kCheckThreads) void k_check(StreamView sv, int64_t x0, int64_t x1, int R, CountsDev cd,
+__global__ __launch_bounds__(kCheckThreads, 4) void k_check(StreamView sv, int64_t x0, int64_t x1, int R, CountsDev cd,
                                                          unsigned long long *__restrict__ bitmap,
                                                          uint32_t *__restrict__ words) {
   constexpr bool EAGER = MODE == MODE_EAGER;
@@ -577,6 +586,8 @@ __global__ __launch_bounds__(kCheckThreads) void k_check(StreamView sv, int64_t 
     __syncthreads();
     const Tile tl{s_win, s_opc, s_nbad, base};
     const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
+    auto run_tile = [&](auto interior_tag) {
+    constexpr bool INTERIOR = decltype(interior_tag)::value;
 #pragma unroll 1
     for (int j = 0; j < kTile / (4 * kCheckThreads); j++) {
       const int g = j * kCheckThreads + threadIdx.x;  // group of 4 consecutive positions
@@ -591,7 +602,7 @@ __global__ __launch_bounds__(kCheckThreads) void k_check(StreamView sv, int64_t 
         int32_t f[8];
 #pragma unroll
         for (int q = 0; q < 8; q++) f[q] = (int32_t)__builtin_amdgcn_alignbyte(W[q + 1], W[q], o);
-        uint32_t w = check_first<EAGER>(tl, sv, lensL, x, 4 * g + o, R, f);
+        uint32_t w = check_first<EAGER, INTERIOR>(tl, sv, lensL, x, 4 * g + o, R, f);
         w = (x >= x0 && x < x1) ? w : W_NONE;
         wd[o] = w;
       }
@@ -629,6 +640,9 @@ __global__ __launch_bounds__(kCheckThreads) void k_check(StreamView sv, int64_t 
       const uint32_t ones = x1a ^ x2a, c3 = x1a & x2a;
       acc.pl.add(ones, c1 ^ c2 ^ c3, (c1 & c2) | (c3 & (c1 ^ c2)));
     }
+    };
+    if (base + kTile + kInteriorTail <= sv.L) run_tile(std::integral_constant<bool, true>{});
+    else run_tile(std::integral_constant<bool, false>{});
     if (COUNTS) {
       if (++since_flush == kFlushTiles) {
         flush_acc(acc, s_acc, lane);
