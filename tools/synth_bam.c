@@ -5,7 +5,10 @@
  * htsjdk-style 65498-byte uncompressed payloads and compressed with zlib level 6 (raw DEFLATE, BGZF header
  * with the BC subfield, CRC32, ISIZE).  Records are NOT block-aligned (they straddle blocks), except that the
  * tile ends on a record boundary, so a file = header blocks + tile × k + EOF marker is a valid BAM whose record
- * chain runs through every tile seam.  Long-read mode (read_len > 1000) gives records that span many blocks.
+ * chain runs through every tile seam.  read_len > 1000 gives fixed-length long reads with a few ops;
+ * read_len == 0 is the long-read config of SURVEY §8(d) #5 (ONT/PacBio-like, bam_long_record): log-normal
+ * lengths 10–50 kb (median 20 kb), 200–3000 CIGAR ops, names up to 63 characters, unpaired, and ~5% of
+ * records larger than a 64 KiB BGZF block.
  *
  * Contig set: the 84 GRCh37 contigs of the reference's 2.bam header (ContigLengthsTest.scala:15-102).
  */
@@ -14,6 +17,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <math.h>
 #include <zlib.h>
 
 #define PAYLOAD 65498
@@ -189,6 +193,92 @@ static void bam_record(buf_t *b, rng_t *r, coord_t *co, int read_len, uint8_t *r
   co->serial++;
 }
 
+/* Long-read record.  Length: 20 kb · exp(0.45·z), z ≈ N(0,1) from 12 uniforms,
+ * clipped to [10 000, 50 000].  CIGAR: soft clips at both ends, then alternating M and I/D ops until
+ * 200–3000 ops; query-consuming ops sum to the read length.  Unpaired (next_refID −1), 0.5% unmapped. */
+static void bam_long_record(buf_t *b, rng_t *r, coord_t *co, uint8_t *rec, uint32_t *cig) {
+  int n = 0;
+  double z = -6.0;
+  for (int i = 0; i < 12; i++) z += (double)(rnext(r) >> 11) * (1.0 / 9007199254740992.0);
+  double lf = 20000.0 * exp(0.45 * z);
+  int read_len = lf < 10000.0 ? 10000 : lf > 50000.0 ? 50000 : (int)lf;
+  char name[80];
+  static const char hex[] = "0123456789abcdef";
+  int ln = 0;
+  for (int i = 0; i < 36; i++) name[ln++] = (i == 8 || i == 13 || i == 18 || i == 23) ? '-' : hex[rnext(r) & 15];
+  const int extra = (int)runi(r, 28); /* names of 36..63 characters */
+  if (extra) {
+    name[ln++] = '_';
+    for (int i = 1; i < extra; i++) name[ln++] = (char)('A' + runi(r, 26));
+  }
+  name[ln] = 0;
+  const int lrn = ln + 1;
+  const int unmapped = runi(r, 1000) < 5;
+  co->pos += (int32_t)runi(r, 400);
+  if (co->pos + 120000 > kLens[co->ref]) { co->ref = (co->ref + 1) % 25; co->pos = 10000; }
+  const int32_t pos = co->pos;
+  int nc = 0, ref_span = 0;
+  if (!unmapped) {
+    int target = 201 + (int)runi(r, 2800);
+    if (target > read_len / 4) target = read_len / 4;
+    const int s1 = 10 + (int)runi(r, 190), s2 = 10 + (int)runi(r, 190);
+    const int pairs = (target - 3) / 2; /* S, M + (I|D) pairs, a final M, S: 2·pairs + 3 <= target ops */
+    int q = read_len - s1 - s2;         /* query bases for M and I ops */
+    cig[nc++] = ((uint32_t)s1 << 4) | 4;
+    for (int k = 0; k < pairs; k++) {
+      const int left = pairs - k;       /* M ops still to place, including this one (+ the final M) */
+      int m = q / (left + 1);
+      m = m < 1 ? 1 : m - 1 + (int)runi(r, 3);
+      if (m > q - left) m = q - left;
+      if (m < 1) m = 1;
+      cig[nc++] = (uint32_t)m << 4;
+      ref_span += m;
+      q -= m;
+      const int l = 1 + (int)runi(r, 4);
+      if (runi(r, 2) && q - l >= left) { cig[nc++] = ((uint32_t)l << 4) | 1; q -= l; }
+      else { cig[nc++] = ((uint32_t)l << 4) | 2; ref_span += l; }
+    }
+    cig[nc++] = (uint32_t)q << 4; /* q >= 1 by construction */
+    ref_span += q;
+    cig[nc++] = ((uint32_t)s2 << 4) | 4;
+  }
+  const uint16_t flag = (uint16_t)(unmapped ? 4 : (runi(r, 2) ? 16 : 0));
+  const uint8_t mapq = unmapped ? 0 : (uint8_t)runi(r, 61);
+  const int bin = reg2bin(pos, pos + (ref_span > 0 ? ref_span : 1));
+  W32(0);
+  W32(co->ref);
+  W32(pos);
+  W8(lrn); W8(mapq); W16(bin);
+  W16(nc); W16(flag);
+  W32(read_len);
+  W32(-1);
+  W32(-1);
+  W32(0);
+  memcpy(rec + n, name, (size_t)lrn); n += lrn;
+  for (int i = 0; i < nc; i++) W32(cig[i]);
+  static const uint8_t codes[4] = {1, 2, 4, 8};
+  for (int i = 0; i < read_len; i += 2) {
+    uint8_t hi = codes[rnext(r) & 3];
+    uint8_t lo = (i + 1 < read_len) ? codes[rnext(r) & 3] : 0;
+    W8((hi << 4) | lo);
+  }
+  uint8_t prevq = 20;
+  for (int i = 0; i < read_len; i++) { /* unbinned qualities 2..41 with runs */
+    if (runi(r, 10) >= 7) prevq = (uint8_t)(2 + runi(r, 40));
+    W8(prevq);
+  }
+  W8('N'); W8('M'); W8('i'); W32(runi(r, 2000));
+  W8('A'); W8('S'); W8('i'); W32(read_len - (int)runi(r, 2000));
+  W8('R'); W8('G'); W8('Z'); memcpy(rec + n, "grp1", 5); n += 5;
+  const uint32_t bs = (uint32_t)(n - 4);
+  memcpy(rec, &bs, 4);
+  bput(b, rec, n);
+  co->serial++;
+}
+#undef W32
+#undef W16
+#undef W8
+
 static void bgzf_block(const uint8_t *src, int len, int level, buf_t *out_blk) {
   uint8_t cbuf[65536 + 1024];
   z_stream zs;
@@ -289,11 +379,14 @@ int64_t synth_tile(uint64_t seed, int64_t target_u, int read_len, int level, int
   buf_t u = {0};
   coord_t co = {0, 10000, seed * 1000003ull};
   int64_t nrec = 0;
-  uint8_t *rec = (uint8_t *)malloc((size_t)(4 * read_len + 4096));
+  uint8_t *rec = (uint8_t *)malloc((size_t)(read_len ? 4 * read_len + 4096 : 4 * 50000 + 4 * 3000 + 4096));
+  uint32_t *cig = (uint32_t *)malloc(4 * 3008);
   while (u.n < target_u) {
-    bam_record(&u, &r, &co, read_len, rec);
+    if (read_len) bam_record(&u, &r, &co, read_len, rec);
+    else bam_long_record(&u, &r, &co, rec, cig);
     nrec++;
   }
+  free(cig);
   free(rec);
   int64_t n = compress_stream(u.p, u.n, level, threads, out);
   if (n_records) *n_records = nrec;
