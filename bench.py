@@ -92,6 +92,13 @@ def main():
                     help="compressed MB of the same synthetic file timed on the CPU oracle (~10 s at 16 threads)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EEDBA11)
+    ap.add_argument("--workload", choices=["full-check", "load-reads"], default="full-check",
+                    help="full-check: BASELINE metric (compute-splits + full-check); load-reads: configs[3] "
+                         "(FindBlockStart → FindRecordStart → record chains → decoded columns)")
+    ap.add_argument("--windows", type=int, default=1,
+                    help="sequential byte-range windows per GPU: streams a shard larger than HBM through one "
+                         "device (each window: its own load + halo; PCIe copy inside the timed step)")
+    ap.add_argument("--read-len", type=int, default=150, help="0 = long-read config (configs[4])")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -114,18 +121,56 @@ def main():
     split_size = int(args.split_mb * (1 << 20))
     t = time.time()
     s = synth.SynthBam.for_size(int(args.size_gb * 1e9 * world), tile_mb=args.tile_mb, seed=args.seed,
-                                threads=args.threads)
-    plans = sdist.plan_shards(s.size, split_size, world)
+                                threads=args.threads, read_len=args.read_len)
+    W = max(1, args.windows)
+    plans = sdist.plan_shards(s.size, split_size, world)  # rank-level plans (what all_gather sees)
     plan = plans[rank]
-    shard = sdist.GpuShard(plan, s.slice, split_size, s.contig_lengths, device=local)
+    wplans = sdist.plan_shards(s.size, split_size, world * W)[rank * W:(rank + 1) * W]
+    shard = sdist.GpuShard(plan, s.slice, split_size, s.contig_lengths, device=local) if W == 1 else None
     log(f"[rank {rank}] synthetic file {s.size / 1e9:.2f} GB ({s.n_records} records), shard "
-        f"[{plan.lo}, {plan.owned_hi}) splits {plan.split_first}+{plan.split_count}, setup {time.time() - t:.1f}s")
+        f"[{plan.lo}, {plan.owned_hi}) splits {plan.split_first}+{plan.split_count} in {W} window(s), "
+        f"workload {args.workload}, setup {time.time() - t:.1f}s")
+    kernels = ("scan", "chain", "inflate", "inflate_decode", "inflate_resolve", "check_full", "check_pass0",
+               "check_chains", "find_record", "records", "load_records")
+    last = {}
+
+    def run_window(sh):
+        if args.workload == "load-reads":
+            sizes = sh.load_step()
+            z = np.zeros(len(sizes), np.int64)
+            r = sdist.ShardResult(np.zeros(sdist.N_COUNT_WORDS, np.int64), z, z, (sizes > 0).astype(np.int64),
+                                  sizes.astype(np.int64))
+        else:
+            r = sh.step()
+        ms = {k: max(sh.f.kernel_ms(k), 0.0) for k in kernels}
+        last.update(U=int(sh.f.uncompressed_size), blocks=sh.f.blocks(), f=sh.f)
+        return r, ms
 
     def step():
-        res = shard.step()
-        if world > 1:
+        if W == 1:
+            res, ms = run_window(shard)
+        else:
+            parts, ms = [], {k: 0.0 for k in kernels}
+            U, nb = 0, 0
+            for wp in wplans:
+                sh = sdist.GpuShard(wp, s.slice, split_size, s.contig_lengths, device=local)
+                try:
+                    r, m = run_window(sh)
+                    U += last["U"]
+                    nb += last["blocks"][0].size
+                finally:
+                    last.pop("f", None)
+                    sh.close()
+                parts.append(r)
+                for k in kernels:
+                    ms[k] += m[k]
+            last.update(U=U, nblocks=nb)
+            res = sdist.ShardResult(np.sum([r.counts for r in parts], axis=0),
+                                    *(np.concatenate([getattr(r, a) for r in parts]) for a in
+                                      ("first_block_pos", "first_offset", "nonempty", "n_records")))
+        if world > 1 and args.workload == "full-check":
             sdist.gather_results(res, plans, device=dev)
-        return res
+        return res, ms
 
     def sync():
         torch.cuda.synchronize(dev)
@@ -134,19 +179,16 @@ def main():
 
     res = None
     for _ in range(args.warmup):
-        res = step()
-    kernels = ("scan", "chain", "inflate", "inflate_decode", "inflate_resolve", "check_full", "check_pass0",
-               "check_chains", "find_record", "records")
+        res, _ = step()
     tot_ms = {k: 0.0 for k in kernels}
     sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
         ts = time.perf_counter()
-        res = step()
+        res, ms = step()
         log(f"[rank {rank}] step {i}: {(time.perf_counter() - ts) * 1e3:.1f} ms (host wall)")
         for k in kernels:
-            ms = shard.f.kernel_ms(k)
-            tot_ms[k] += max(ms, 0.0)
+            tot_ms[k] += ms[k]
     sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -155,9 +197,10 @@ def main():
         elapsed = float(tt.item())
 
     # --- size-independent parity properties of the last step (full sizes; fixtures cover exactness)
-    f = shard.f
     counts = sdist.unpack_counts(res.counts)
     n_rec = int(res.n_records.sum())
+    if args.workload == "load-reads":  # no checker pass in this workload: the record count is the property
+        counts["n_success"] = n_rec
     ok_local = counts["n_success"] == int(res.n_records.sum()) if world == 1 else True
     if world > 1:
         v = torch.tensor([counts["n_success"], n_rec], dtype=torch.int64, device=dev)
@@ -173,26 +216,35 @@ def main():
     # --- roofline of the dominant kernel (this rank's shard; per launch).  Candidates are single kernels:
     # k_check<0> (record-0 pass: reads U, writes the U/8 PASS0 bitmap), k_inflate_decode (reads the C payload;
     # its token stream is an internal intermediate) and k_inflate_resolve (writes U; tokens internal).
-    st, cs, us, uo = f.blocks()
-    comp_payload = int(cs.astype(np.int64).sum())
-    U = int(f.uncompressed_size)
+    U = last["U"]
+    if W == 1:
+        st, cs, us, uo = last["blocks"]
+        comp_payload = int(cs.astype(np.int64).sum())
+        nblocks = int(st.size)
+    else:  # per-window launches; the roofline uses the summed window times and bytes
+        comp_payload = plan.owned_hi - plan.lo
+        nblocks = last["nblocks"]
     avg = {k: tot_ms[k] / args.steps for k in kernels}
     alg = {"check_pass0": U + U // 8, "inflate_decode": comp_payload, "inflate_resolve": U}
     names = {"check_pass0": "k_check<0>", "inflate_decode": "k_inflate_decode", "inflate_resolve": "k_inflate_resolve"}
+    if args.workload == "load-reads":
+        del alg["check_pass0"]
     dom = max(alg, key=lambda k: avg[k])
     achieved = alg[dom] / (avg[dom] * 1e-3) / 1e9 if avg[dom] > 0 else 0.0
-    traffic = measured_traffic(names[dom], args)
+    traffic = measured_traffic(names[dom], args) if (args.read_len == 150 and W == 1) else None
 
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.workload == "full-check" and args.read_len == 150:
             try:
                 cpu = cpu_baseline(args.cpu_sample_mb, args.threads, split_size, args.seed)
             except Exception as e:  # reported, never substituted for the GPU number
                 log(f"cpu baseline failed: {e!r}")
         value = s.size * args.steps / elapsed / 1e9
+        fc = args.workload == "full-check"
         line = {
-            "metric": "compressed BAM GB/s for compute-splits + full-check (whole node, 1/2/4/8 GPU)",
+            "metric": "compressed BAM GB/s for compute-splits + full-check (whole node, 1/2/4/8 GPU)" if fc else
+                      "compressed BAM GB/s for loadReads record decode (whole node, 1/2/4/8 GPU)",
             "value": round(value, 3),
             "unit": "GB/s",
             "n_gpus": world,
@@ -203,12 +255,18 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (tools/synth_bam.c: 150bp paired Illumina-like, zlib-6 BGZF, seed %#x)" % args.seed,
-            "config": {"workload": "Synthetic %.0f GB Illumina-like BAM per GPU: compute-splits @ %g MiB + "
-                                   "full-check of every uncompressed offset" % (args.size_gb, args.split_mb),
+            "data": "synthetic (tools/synth_bam.c: %s, zlib-6 BGZF, seed %#x)" % (
+                "150bp paired Illumina-like" if args.read_len == 150 else "long-read 10-50 kb" if args.read_len == 0
+                else f"{args.read_len} bp", args.seed),
+            "config": {"workload": ("Synthetic %.0f GB %s BAM per GPU: " % (
+                                   args.size_gb, "Illumina-like" if args.read_len == 150 else
+                                   "long-read" if args.read_len == 0 else f"{args.read_len} bp")) +
+                                   ("compute-splits @ %g MiB + full-check of every uncompressed offset" % args.split_mb
+                                    if fc else "loadReads @ %g MiB splits: records decoded into device columns"
+                                    % args.split_mb),
                        "file_gb": round(s.size / 1e9, 3), "uncompressed_gb_per_gpu": round(U / 1e9, 3),
-                       "records": s.n_records, "blocks_per_gpu": int(st.size), "split_mb": args.split_mb,
-                       "parallelism": f"shard{world}"},
+                       "records": s.n_records, "blocks_per_gpu": nblocks, "split_mb": args.split_mb,
+                       "windows_per_gpu": W, "parallelism": f"shard{world}"},
             "uncompressed_gbps": round(U * world * args.steps / elapsed / 1e9, 3),
             "kernel_ms": {k: round(v, 3) for k, v in avg.items()},
             "roofline": {"bound": "hbm", "kernel": names[dom], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
@@ -222,7 +280,8 @@ def main():
             "parity": parity,
         }
         print(json.dumps(line), flush=True)
-    shard.close()
+    if shard is not None:
+        shard.close()
     if world > 1:
         dist.destroy_process_group()
 

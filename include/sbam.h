@@ -176,9 +176,43 @@ int sbam_compute_splits(sbam_ctx *ctx, const sbam_split_args *args, sbam_split *
  * (cap entries) and *n_out records; record bytes are stream[off, off+4+block_size). */
 int sbam_record_offsets(sbam_ctx *ctx, int64_t x0, int64_t x_end, int64_t *offsets, int64_t cap, int64_t *n_out);
 
+/* ---- record decode: loadReads / loadReadsAndPositions (CanLoadBam.scala:221-241, 281-334) ------------- */
+
+/* Per-record columns: the record's flat stream offset, its Pos, and the BAM fixed fields (SAM spec §4.2, the
+ * part htsjdk BAMRecordCodec.decode reads eagerly: RecordStream.scala:16-33).  Record bytes are
+ * stream[offset, offset + 4 + block_size) (sbam_read_uncompressed).  Any pointer may be NULL (not copied). */
+typedef struct {
+  int64_t *offset;
+  int64_t *block_pos;   /* Pos.blockPos */
+  int32_t *block_off;   /* Pos.offset   */
+  int32_t *block_size;
+  int32_t *ref_id;
+  int32_t *pos;
+  uint32_t *bin_mq_nl;  /* bin << 16 | MAPQ << 8 | l_read_name */
+  uint32_t *flag_nc;    /* FLAG << 16 | n_cigar_op */
+  int32_t *l_seq;
+  int32_t *next_ref_id;
+  int32_t *next_pos;
+  int32_t *tlen;
+} sbam_record_columns;
+
+/* Records of Hadoop splits [first, first+count) — the partitions of loadReadsAndPositions, in split order —
+ * decoded into device-resident columns owned by ctx (valid until the next load, reset or close).
+ * split_counts[count] (may be NULL) receives the partition sizes, *n_records their sum.  With
+ * use_success_bitmap and a preceding full check over the range, the chains are proven equal to the checker's
+ * success bitmap and listed in parallel; otherwise (or when the proof fails) each split's chain is walked. */
+int sbam_load_records(sbam_ctx *ctx, const sbam_split_args *args, int64_t first, int64_t count, int64_t *split_counts,
+                      int64_t *n_records);
+
+/* Copy records [i0, i0+n) of the last sbam_load_records into caller-owned host columns. */
+int sbam_get_record_columns(sbam_ctx *ctx, int64_t i0, int64_t n, const sbam_record_columns *out);
+
+/* Device pointers of the last sbam_load_records' columns (for in-process GPU consumers; no copy). */
+int sbam_record_columns_device(sbam_ctx *ctx, sbam_record_columns *dev, int64_t *n_records);
+
 /* ---- timing support for bench/profiling -------------------------------------------------------- */
 /* Device time (ms, HIP events on the library's stream) of the most recent launch of a named kernel
- * family: "scan", "inflate", "check_full", "check_eager", "records". Returns -1 if none. */
+ * family: "scan", "inflate", "check_full", "check_eager", "records", "load_records". Returns -1 if none. */
 double sbam_last_kernel_ms(sbam_ctx *ctx, const char *kernel);
 
 #ifdef __cplusplus

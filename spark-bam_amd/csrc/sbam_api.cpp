@@ -62,6 +62,16 @@ struct sbam_ctx {
   int32_t *d_blkpage = nullptr;
   size_t blkpage_cap = 0;
   unsigned int *d_icnt = nullptr;  // decode work, pool pages used, resolve work
+  // split chains: per-split first record / chain end / count / record base (grow-only)
+  int64_t *d_sx = nullptr, *d_se = nullptr, *d_sn = nullptr, *d_sb = nullptr;
+  size_t sx_cap = 0, se_cap = 0, sn_cap = 0, sb_cap = 0;
+  // decoded records of the last sbam_load_records (offset column + RecordColumnsDev in one arena)
+  int64_t *d_roff = nullptr;
+  size_t roff_cap = 0;
+  uint8_t *d_rcols = nullptr;
+  size_t rcols_cap = 0;
+  RecordColumnsDev rcols{};
+  int64_t n_loaded = -1;
   // small device scratch
   int64_t *d_small = nullptr;  // 64 int64
   unsigned long long *d_counts = nullptr;
@@ -242,6 +252,12 @@ void sbam_close(sbam_ctx *c) {
   dfree(c->d_icnt);
   dfree(c->d_small);
   dfree(c->d_counts);
+  dfree(c->d_sx);
+  dfree(c->d_se);
+  dfree(c->d_sn);
+  dfree(c->d_sb);
+  dfree(c->d_roff);
+  dfree(c->d_rcols);
   for (auto &kv : c->ev) {
     (void)hipEventDestroy(kv.second.first);
     (void)hipEventDestroy(kv.second.second);
@@ -258,6 +274,7 @@ int sbam_reset(sbam_ctx *c) {
   c->nblocks = -1;
   c->L = -1;
   c->bm_valid = false;
+  c->n_loaded = -1;
   c->err = sbam_error{};
   return SBAM_OK;
 }
@@ -787,21 +804,20 @@ int sbam_file_splits(int64_t file_size, int64_t split_size, int64_t *starts, int
   return SBAM_OK;
 }
 
-int sbam_split_records(sbam_ctx *c, const sbam_split_args *a, int64_t first, int64_t count, sbam_pos *first_pos,
-                       int32_t *found, int64_t *n_records) {
-  if (!c || !a || first < 0 || count < 0) return SBAM_ERR_ARG;
-  int rc = ensure_stream(c);
-  if (rc) return rc;
-  HIPCHK(c, hipSetDevice(c->device));
+// FindBlockStart → FindRecordStart for Hadoop splits [first, first+count): first-record offsets xs and chain
+// ends xe = offset of Pos(split end, 0) (CanLoadBam.scala:195-241).
+static int split_starts(sbam_ctx *c, const sbam_split_args *a, int64_t first, int64_t count, std::vector<int64_t> &xs,
+                        std::vector<int64_t> &xe) {
   int64_t ns = 0;
   sbam_file_splits(c->file_size, a->split_size, nullptr, nullptr, 0, &ns);
   if (first + count > ns) return set_err(c, SBAM_ERR_ARG, "split range past %lld splits", (long long)ns);
   std::vector<int64_t> st(ns), en(ns);
   sbam_file_splits(c->file_size, a->split_size, st.data(), en.data(), ns, &ns);
   std::vector<int64_t> q(st.begin() + first, st.begin() + first + count), bs(count);
-  rc = sbam_find_block_starts(c, q.data(), count, a->bgzf_blocks_to_check, bs.data());
+  int rc = sbam_find_block_starts(c, q.data(), count, a->bgzf_blocks_to_check, bs.data());
   if (rc) return rc;
-  std::vector<int64_t> x0(count), xe(count);
+  std::vector<int64_t> x0(count);
+  xe.assign(count, 0);
   for (int64_t i = 0; i < count; i++) {
     const int64_t b = block_at(c, bs[i] - c->base);
     if (b < 0) {  // FindRecordStart on the EOF marker: empty stream → None → NoReadFoundException
@@ -812,7 +828,6 @@ int sbam_split_records(sbam_ctx *c, const sbam_split_args *a, int64_t first, int
     x0[i] = c->h_buoff[b];
     xe[i] = x_end_of(c, en[first + i] - c->base);
   }
-  std::vector<int64_t> xs;
   rc = find_record_starts(c, x0, a->reads_to_check, a->max_read_size, a->use_success_bitmap != 0, xs);
   if (rc) return rc;
   for (int64_t i = 0; i < count; i++) {
@@ -823,25 +838,64 @@ int sbam_split_records(sbam_ctx *c, const sbam_split_args *a, int64_t first, int
                      a->max_read_size, "path", (long long)bs[i]);
     }
   }
-  int64_t *d_x = nullptr, *d_e = nullptr, *d_n = nullptr;
-  HIPCHK(c, dalloc(&d_x, count));
-  HIPCHK(c, dalloc(&d_e, count));
-  HIPCHK(c, dalloc(&d_n, count));
-  HIPCHK(c, hipMemcpyAsync(d_x, xs.data(), count * 8, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(d_e, xe.data(), count * 8, hipMemcpyHostToDevice, c->stream));
-  {
-    Timer t(c, "records");
-    HIPCHK(c, launch_record_counts(view(c), d_x, d_e, count, d_n, c->stream));
+  return SBAM_OK;
+}
+
+// Record counts of the chains [xs[i], xe[i]) (RecordStream.scala:27-41).  With try_bitmap and a success bitmap
+// covering them, the chains are proven equal to the bitmap's set bits (sbam_records.hip) and counted by
+// popcount; else (or if the proof fails) each chain is walked.  Leaves xs/xe on the device (d_sx, d_se).
+static int split_counts(sbam_ctx *c, bool try_bitmap, const std::vector<int64_t> &xs, const std::vector<int64_t> &xe,
+                        std::vector<int64_t> &cnt, bool *proved) {
+  const int64_t n = (int64_t)xs.size();
+  *proved = false;
+  cnt.assign(n, 0);
+  if (!n) return SBAM_OK;
+  HIPCHK(c, ensure(&c->d_sx, &c->sx_cap, n));
+  HIPCHK(c, ensure(&c->d_se, &c->se_cap, n));
+  HIPCHK(c, ensure(&c->d_sn, &c->sn_cap, n));
+  HIPCHK(c, hipMemcpyAsync(c->d_sx, xs.data(), n * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->d_se, xe.data(), n * 8, hipMemcpyHostToDevice, c->stream));
+  const int64_t X0 = *std::min_element(xs.begin(), xs.end());
+  const int64_t X1 = *std::max_element(xe.begin(), xe.end());
+  Timer t(c, "records");
+  if (try_bitmap && c->bm_valid && X0 >= c->bm_x0 && X1 <= c->bm_x1) {
+    int32_t *d_fail = reinterpret_cast<int32_t *>(c->d_small + 8);
+    const int64_t xa = c->bm_x0 & ~(int64_t)63;
+    HIPCHK(c, hipMemsetAsync(d_fail, 0, 4, c->stream));
+    HIPCHK(c, launch_chain_proof(c->d_u, c->L, c->d_bitmap, xa, X0, X1, d_fail, c->stream));
+    HIPCHK(c, launch_split_popcounts(c->d_bitmap, xa, c->d_sx, c->d_se, n, c->d_sn, d_fail, c->stream));
+    int32_t fail = 1;
+    HIPCHK(c, hipMemcpyAsync(&fail, d_fail, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(cnt.data(), c->d_sn, n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (!fail) {
+      *proved = true;
+      return SBAM_OK;
+    }
   }
-  std::vector<int64_t> cnt(count);
-  HIPCHK(c, hipMemcpyAsync(cnt.data(), d_n, count * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, launch_record_counts(view(c), c->d_sx, c->d_se, n, c->d_sn, c->stream));
+  HIPCHK(c, hipMemcpyAsync(cnt.data(), c->d_sn, n * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  dfree(d_x);
-  dfree(d_e);
-  dfree(d_n);
-  for (int64_t i = 0; i < count; i++) {
+  for (int64_t i = 0; i < n; i++) {
     if (cnt[i] == -2) return set_err(c, SBAM_ERR_HALO, "record chain left the shard");
     if (cnt[i] < 0) return set_err(c, SBAM_ERR_INFLATE, "UnexpectedEOF in record stream");
+  }
+  return SBAM_OK;
+}
+
+int sbam_split_records(sbam_ctx *c, const sbam_split_args *a, int64_t first, int64_t count, sbam_pos *first_pos,
+                       int32_t *found, int64_t *n_records) {
+  if (!c || !a || first < 0 || count < 0) return SBAM_ERR_ARG;
+  int rc = ensure_stream(c);
+  if (rc) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  std::vector<int64_t> xs, xe, cnt;
+  rc = split_starts(c, a, first, count, xs, xe);
+  if (rc) return rc;
+  bool proved = false;
+  rc = split_counts(c, a->use_success_bitmap != 0, xs, xe, cnt, &proved);
+  if (rc) return rc;
+  for (int64_t i = 0; i < count; i++) {
     if (first_pos) first_pos[i] = pos_of(c, xs[i]);
     if (found) found[i] = cnt[i] > 0;
     if (n_records) n_records[i] = cnt[i];
@@ -885,6 +939,90 @@ int sbam_record_offsets(sbam_ctx *c, int64_t x0, int64_t x_end, int64_t *offsets
   if (offsets && n) HIPCHK(c, hipMemcpy(offsets, d_o, std::min(n, cap) * 8, hipMemcpyDeviceToHost));
   dfree(d_o);
   *n_out = n;
+  return SBAM_OK;
+}
+
+// ---- record decode ---------------------------------------------------------------------------------------
+int sbam_load_records(sbam_ctx *c, const sbam_split_args *a, int64_t first, int64_t count, int64_t *split_counts_out,
+                      int64_t *n_records) {
+  if (!c || !a || first < 0 || count < 0) return SBAM_ERR_ARG;
+  int rc = ensure_stream(c);
+  if (rc) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  c->n_loaded = -1;
+  std::vector<int64_t> xs, xe, cnt;
+  rc = split_starts(c, a, first, count, xs, xe);
+  if (rc) return rc;
+  bool proved = false;
+  rc = split_counts(c, a->use_success_bitmap != 0, xs, xe, cnt, &proved);
+  if (rc) return rc;
+  std::vector<int64_t> base(count + 1, 0);
+  for (int64_t i = 0; i < count; i++) base[i + 1] = base[i] + cnt[i];
+  const int64_t N = base[count];
+  HIPCHK(c, ensure(&c->d_sb, &c->sb_cap, count + 1));
+  HIPCHK(c, ensure(&c->d_roff, &c->roff_cap, N));
+  // column arena: block_pos (8 B) + 10 × 4 B, each column 256-B aligned
+  const size_t stride = ((size_t)std::max<int64_t>(N, 1) * 8 + 255) & ~(size_t)255;
+  const size_t stride4 = ((size_t)std::max<int64_t>(N, 1) * 4 + 255) & ~(size_t)255;
+  HIPCHK(c, ensure(&c->d_rcols, &c->rcols_cap, stride + 10 * stride4));
+  {
+    uint8_t *p = c->d_rcols;
+    RecordColumnsDev &k = c->rcols;
+    k.block_pos = reinterpret_cast<int64_t *>(p);
+    int32_t *q[10];
+    for (int j = 0; j < 10; j++) q[j] = reinterpret_cast<int32_t *>(p + stride + j * stride4);
+    k.block_off = q[0]; k.block_size = q[1]; k.ref_id = q[2]; k.pos = q[3];
+    k.bin_mq_nl = reinterpret_cast<uint32_t *>(q[4]); k.flag_nc = reinterpret_cast<uint32_t *>(q[5]);
+    k.l_seq = q[6]; k.next_ref_id = q[7]; k.next_pos = q[8]; k.tlen = q[9];
+  }
+  HIPCHK(c, hipMemcpyAsync(c->d_sb, base.data(), (count + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  {
+    Timer t(c, "load_records");
+    if (proved)
+      HIPCHK(c, launch_split_offsets(c->d_bitmap, c->bm_x0 & ~(int64_t)63, c->d_sx, c->d_se, c->d_sb, count, c->d_roff,
+                                     c->stream));
+    else
+      HIPCHK(c, launch_record_walk(c->d_u, c->L, c->d_sx, c->d_se, c->d_sb, count, c->d_roff, c->stream));
+    HIPCHK(c, launch_record_columns(c->d_u, c->d_roff, N, c->d_bstart, c->d_buoff, c->d_bu, c->nblocks, c->base,
+                                    c->rcols, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->n_loaded = N;
+  if (split_counts_out)
+    for (int64_t i = 0; i < count; i++) split_counts_out[i] = cnt[i];
+  if (n_records) *n_records = N;
+  return SBAM_OK;
+}
+
+int sbam_get_record_columns(sbam_ctx *c, int64_t i0, int64_t n, const sbam_record_columns *o) {
+  if (!c || !o || i0 < 0 || n < 0) return SBAM_ERR_ARG;
+  if (c->n_loaded < 0) return set_err(c, SBAM_ERR_STATE, "sbam_load_records has not run");
+  if (i0 + n > c->n_loaded)
+    return set_err(c, SBAM_ERR_ARG, "records [%lld, %lld) past %lld loaded", (long long)i0, (long long)(i0 + n),
+                   (long long)c->n_loaded);
+  if (!n) return SBAM_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  const RecordColumnsDev &k = c->rcols;
+  struct { void *dst; const void *src; size_t w; } cp[] = {
+      {o->offset, c->d_roff, 8}, {o->block_pos, k.block_pos, 8}, {o->block_off, k.block_off, 4},
+      {o->block_size, k.block_size, 4}, {o->ref_id, k.ref_id, 4}, {o->pos, k.pos, 4},
+      {o->bin_mq_nl, k.bin_mq_nl, 4}, {o->flag_nc, k.flag_nc, 4}, {o->l_seq, k.l_seq, 4},
+      {o->next_ref_id, k.next_ref_id, 4}, {o->next_pos, k.next_pos, 4}, {o->tlen, k.tlen, 4}};
+  for (auto &e : cp)
+    if (e.dst)
+      HIPCHK(c, hipMemcpyAsync(e.dst, static_cast<const uint8_t *>(e.src) + i0 * e.w, n * e.w, hipMemcpyDeviceToHost,
+                               c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SBAM_OK;
+}
+
+int sbam_record_columns_device(sbam_ctx *c, sbam_record_columns *d, int64_t *n_records) {
+  if (!c || !d) return SBAM_ERR_ARG;
+  if (c->n_loaded < 0) return set_err(c, SBAM_ERR_STATE, "sbam_load_records has not run");
+  const RecordColumnsDev &k = c->rcols;
+  *d = sbam_record_columns{c->d_roff, k.block_pos, k.block_off, k.block_size, k.ref_id, k.pos,
+                           k.bin_mq_nl, k.flag_nc, k.l_seq, k.next_ref_id, k.next_pos, k.tlen};
+  if (n_records) *n_records = c->n_loaded;
   return SBAM_OK;
 }
 

@@ -44,6 +44,14 @@ struct CountsDev {  // mirrors sbam_counts (int64 fields) in device memory
   unsigned long long *totals;   // [19] per-flag totals over every counted position
 };
 
+// Device columns of decoded records (sbam_records.hip); mirrors sbam_record_columns minus the offsets.
+struct RecordColumnsDev {
+  int64_t *block_pos;
+  int32_t *block_off, *block_size, *ref_id, *pos;
+  uint32_t *bin_mq_nl, *flag_nc;
+  int32_t *l_seq, *next_ref_id, *next_pos, *tlen;
+};
+
 constexpr int kScanChunk = 1 << 20;  // bytes per workgroup in the BGZF candidate scan
 constexpr int kInflateScratchU16 = 2048;  // per-lane Huffman table scratch (u16 entries)
 constexpr int kStreamPad = 16384;  // zero pad behind the uncompressed stream (>= checker LDS window)
@@ -92,5 +100,18 @@ hipError_t launch_record_counts(StreamView sv, const int64_t *x0, const int64_t 
                                 hipStream_t s);
 hipError_t launch_record_offsets(StreamView sv, int64_t x0, int64_t x_end, int64_t *offsets, int64_t cap,
                                  int64_t *n_out, hipStream_t s);
+// Record chains of splits and record decode (sbam_records.hip).  Bitmaps as for the checker: bit (x - xa) = call
+// at x, xa 64-aligned.  fail: i32 device flag, set to 1 when the chain is not the bitmap's set bits.
+hipError_t launch_chain_proof(const uint8_t *u, int64_t L, const unsigned long long *bm, int64_t xa, int64_t X0,
+                              int64_t X1, int32_t *fail, hipStream_t s);
+hipError_t launch_split_popcounts(const unsigned long long *bm, int64_t xa, const int64_t *xs, const int64_t *xe,
+                                  int64_t n, int64_t *counts, int32_t *fail, hipStream_t s);
+hipError_t launch_split_offsets(const unsigned long long *bm, int64_t xa, const int64_t *xs, const int64_t *xe,
+                                const int64_t *base, int64_t n, int64_t *out, hipStream_t s);
+hipError_t launch_record_walk(const uint8_t *u, int64_t L, const int64_t *xs, const int64_t *xe, const int64_t *base,
+                              int64_t n, int64_t *out, hipStream_t s);
+hipError_t launch_record_columns(const uint8_t *u, const int64_t *offs, int64_t n, const int64_t *bstart,
+                                 const int64_t *buoff, const int32_t *busize, int64_t nblocks, int64_t file_base,
+                                 RecordColumnsDev cols, hipStream_t s);
 
 }  // namespace sbam

@@ -1,0 +1,246 @@
+// sbam_records.hip — record chains of Hadoop splits and their decode into columns (gfx950).
+//
+// Reference: RecordStream._advance (check/src/main/scala/org/hammerlab/bam/iterator/RecordStream.scala:27-41)
+// walks a split's records by block_size alone, from FindRecordStart's Pos while Pos < Pos(split end, 0)
+// (CanLoadBam.scala:221-241, 281-334); htsjdk BAMRecordCodec.decode then reads the 32 fixed bytes after
+// block_size.  A chain is inherently serial (one dependent 4-byte load per record), so a split walked by one
+// lane is latency-bound.  When the full checker has left its success bitmap over the range, the chain is
+// instead PROVEN equal to the bitmap's set bits in parallel, and the per-split record lists come from
+// popcounts and a scan:
+//
+//   chain == set bits of [X0, X1)   ⇔   X0 is set, and for every set bit p in [X0, X1):
+//                                        q = p + 4 + block_size(p) is in (p, L], and the bits in (p, min(q, X1))
+//                                        are all clear, and bit q is set when q < X1.
+//
+// (⇐: starting at X0 every hop lands on the next set bit, so the walk visits exactly the set bits, in order.)
+// Any violation — a false-positive call off the chain, a chain record the checker rejected, a record past EOF —
+// clears the proof and the host falls back to the serial walk, which also reports the reference's errors.
+// Each bitmap word is read about twice and each record's block_size once, so the proof costs a few ms at
+// 10 GB where the serial walk costs ~12.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sbam_internal.h"
+
+namespace sbam {
+
+#define SB_DEV __device__ __forceinline__
+
+namespace {
+
+SB_DEV int32_t rd_i32(const uint8_t *u, int64_t x) {
+  return (int32_t)((uint32_t)u[x] | ((uint32_t)u[x + 1] << 8) | ((uint32_t)u[x + 2] << 16) |
+                   ((uint32_t)u[x + 3] << 24));
+}
+
+// bit at stream offset x of a bitmap whose bit 0 is offset xa (xa 64-aligned)
+SB_DEV bool bm_test(const unsigned long long *bm, int64_t xa, int64_t x) {
+  const int64_t r = x - xa;
+  return (bm[r >> 6] >> (r & 63)) & 1ull;
+}
+
+// any set bit in stream offsets [a, b)?
+SB_DEV bool bm_any(const unsigned long long *bm, int64_t xa, int64_t a, int64_t b) {
+  if (a >= b) return false;
+  int64_t ra = a - xa, rb = b - xa;
+  int64_t wa = ra >> 6, wb = (rb - 1) >> 6;
+  const unsigned long long lo = ~0ull << (ra & 63);
+  const unsigned long long hi = ~0ull >> (63 - ((rb - 1) & 63));
+  if (wa == wb) return (bm[wa] & lo & hi) != 0;
+  if (bm[wa] & lo) return true;
+  for (int64_t w = wa + 1; w < wb; w++)
+    if (bm[w]) return true;
+  return (bm[wb] & hi) != 0;
+}
+
+}  // namespace
+
+// One thread per bitmap word of [X0, X1): every set bit p in it must hop to the next set bit (or past X1).
+__global__ void k_chain_proof(const uint8_t *__restrict__ u, int64_t L, const unsigned long long *__restrict__ bm,
+                              int64_t xa, int64_t X0, int64_t X1, int32_t *__restrict__ fail) {
+  const int64_t w0 = (X0 - xa) >> 6, w1 = (X1 - 1 - xa) >> 6;
+  for (int64_t w = w0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w <= w1;
+       w += (int64_t)gridDim.x * blockDim.x) {
+    unsigned long long m = bm[w];
+    const int64_t base = xa + (w << 6);
+    if (base < X0) m &= ~0ull << (X0 - base);
+    if (base + 64 > X1) m &= (X1 - base >= 64) ? ~0ull : ((1ull << (X1 - base)) - 1);
+    bool bad = false;
+    while (m && !bad) {
+      const int64_t p = base + __builtin_ctzll(m);
+      m &= m - 1;
+      if (p + 4 > L) { bad = true; break; }
+      const int32_t bs = rd_i32(u, p);
+      const int64_t q = p + 4 + (int64_t)bs;
+      if (bs < 0 || q > L) { bad = true; break; }
+      const int64_t e = q < X1 ? q : X1;
+      if (bm_any(bm, xa, p + 1, e)) bad = true;
+      else if (q < X1 && !bm_test(bm, xa, q)) bad = true;
+    }
+    if (bad) atomicOr(fail, 1);
+  }
+}
+
+// One workgroup per split: number of set bits in [xs, xe) (0 for xs < 0); fail unless xs itself is set.
+__global__ void k_split_popcounts(const unsigned long long *__restrict__ bm, int64_t xa, const int64_t *__restrict__ xs,
+                                  const int64_t *__restrict__ xe, int64_t n, int64_t *__restrict__ counts,
+                                  int32_t *__restrict__ fail) {
+  __shared__ unsigned long long part[8];
+  const int64_t i = blockIdx.x;
+  if (i >= n) return;
+  const int64_t a = xs[i], b = xe[i];
+  unsigned long long c = 0;
+  if (a >= 0 && a < b) {
+    const int64_t ra = a - xa, rb = b - xa;
+    const int64_t wa = ra >> 6, wb = (rb - 1) >> 6;
+    for (int64_t w = wa + threadIdx.x; w <= wb; w += blockDim.x) {
+      unsigned long long m = bm[w];
+      if (w == wa) m &= ~0ull << (ra & 63);
+      if (w == wb) m &= ~0ull >> (63 - ((rb - 1) & 63));
+      c += __popcll(m);
+    }
+    if (threadIdx.x == 0 && !bm_test(bm, xa, a)) atomicOr(fail, 1);
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); k++) t += part[k];
+    counts[i] = (int64_t)t;
+  }
+}
+
+// One workgroup (256 threads) per split: offsets of the set bits of [xs, xe) at out[base[i] ...], in order.
+__global__ void __launch_bounds__(256) k_split_offsets(const unsigned long long *__restrict__ bm, int64_t xa,
+                                                       const int64_t *__restrict__ xs, const int64_t *__restrict__ xe,
+                                                       const int64_t *__restrict__ base, int64_t n,
+                                                       int64_t *__restrict__ out) {
+  __shared__ uint32_t wsum[4];
+  const int64_t i = blockIdx.x;
+  if (i >= n) return;
+  const int64_t a = xs[i], b = xe[i];
+  if (a < 0 || a >= b) return;
+  const int64_t ra = a - xa, rb = b - xa;
+  const int64_t wa = ra >> 6, wb = (rb - 1) >> 6;
+  int64_t run = base[i];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int64_t w0 = wa; w0 <= wb; w0 += 256) {
+    const int64_t w = w0 + threadIdx.x;
+    unsigned long long m = 0;
+    if (w <= wb) {
+      m = bm[w];
+      if (w == wa) m &= ~0ull << (ra & 63);
+      if (w == wb) m &= ~0ull >> (63 - ((rb - 1) & 63));
+    }
+    const uint32_t pc = (uint32_t)__popcll(m);
+    // inclusive scan across the wave, then across the 4 waves
+    uint32_t s = pc;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(s, o);
+      if (lane >= o) s += t;
+    }
+    if (lane == 63) wsum[wv] = s;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+    for (int k = 0; k < 4; k++) {
+      if (k < wv) before += wsum[k];
+      total += wsum[k];
+    }
+    int64_t o = run + before + s - pc;
+    const int64_t bx = xa + (w << 6);
+    while (m) {
+      out[o++] = bx + __builtin_ctzll(m);
+      m &= m - 1;
+    }
+    run += total;
+    __syncthreads();
+  }
+}
+
+// Serial fallback: one lane per split walks its chain, writing offsets at out[base[i] ...].
+__global__ void k_record_walk(const uint8_t *__restrict__ u, int64_t L, const int64_t *__restrict__ xs,
+                              const int64_t *__restrict__ xe, const int64_t *__restrict__ base, int64_t n,
+                              int64_t *__restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int64_t x = xs[i], o = base[i];
+  if (x < 0) return;
+  const int64_t end = xe[i];
+  while (x < end && x + 4 <= L) {
+    const int32_t bs = rd_i32(u, x);
+    if (bs < 0 || x + 4 + (int64_t)bs > L) break;  // the count pass already reported this chain's error
+    out[o++] = x;
+    x += 4 + (int64_t)bs;
+  }
+}
+
+// One thread per record: Pos and the fixed fields (BAM spec §4.2; BAMRecordCodec.decode's fixed part) as columns.
+__global__ void k_record_columns(const uint8_t *__restrict__ u, const int64_t *__restrict__ offs, int64_t n,
+                                 const int64_t *__restrict__ bstart, const int64_t *__restrict__ buoff,
+                                 const int32_t *__restrict__ busize, int64_t nblocks, int64_t file_base,
+                                 RecordColumnsDev cols) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t x = offs[i];
+  // Pos: last block with uoff <= x, advanced past zero-length blocks (UncompressedBytes.scala:17-19)
+  int64_t lo = 0, hi = nblocks;  // first block with uoff > x
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (buoff[mid] <= x) lo = mid + 1;
+    else hi = mid;
+  }
+  int64_t b = lo - 1;
+  while (b + 1 < nblocks && x >= buoff[b] + busize[b]) b++;
+  cols.block_pos[i] = file_base + bstart[b];
+  cols.block_off[i] = (int32_t)(x - buoff[b]);
+  uint32_t f[9];
+  for (int k = 0; k < 9; k++) f[k] = (uint32_t)rd_i32(u, x + 4 * k);
+  cols.block_size[i] = (int32_t)f[0];
+  cols.ref_id[i] = (int32_t)f[1];
+  cols.pos[i] = (int32_t)f[2];
+  cols.bin_mq_nl[i] = f[3];
+  cols.flag_nc[i] = f[4];
+  cols.l_seq[i] = (int32_t)f[5];
+  cols.next_ref_id[i] = (int32_t)f[6];
+  cols.next_pos[i] = (int32_t)f[7];
+  cols.tlen[i] = (int32_t)f[8];
+}
+
+hipError_t launch_chain_proof(const uint8_t *u, int64_t L, const unsigned long long *bm, int64_t xa, int64_t X0,
+                              int64_t X1, int32_t *fail, hipStream_t s) {
+  if (X1 <= X0) return hipSuccess;
+  const int64_t words = ((X1 - 1 - xa) >> 6) - ((X0 - xa) >> 6) + 1;
+  int64_t g = (words + 255) / 256;
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(k_chain_proof, dim3((unsigned)g), dim3(256), 0, s, u, L, bm, xa, X0, X1, fail);
+  return hipGetLastError();
+}
+hipError_t launch_split_popcounts(const unsigned long long *bm, int64_t xa, const int64_t *xs, const int64_t *xe,
+                                  int64_t n, int64_t *counts, int32_t *fail, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_split_popcounts, dim3((unsigned)n), dim3(256), 0, s, bm, xa, xs, xe, n, counts, fail);
+  return hipGetLastError();
+}
+hipError_t launch_split_offsets(const unsigned long long *bm, int64_t xa, const int64_t *xs, const int64_t *xe,
+                                const int64_t *base, int64_t n, int64_t *out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_split_offsets, dim3((unsigned)n), dim3(256), 0, s, bm, xa, xs, xe, base, n, out);
+  return hipGetLastError();
+}
+hipError_t launch_record_walk(const uint8_t *u, int64_t L, const int64_t *xs, const int64_t *xe, const int64_t *base,
+                              int64_t n, int64_t *out, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_record_walk, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, u, L, xs, xe, base, n, out);
+  return hipGetLastError();
+}
+hipError_t launch_record_columns(const uint8_t *u, const int64_t *offs, int64_t n, const int64_t *bstart,
+                                 const int64_t *buoff, const int32_t *busize, int64_t nblocks, int64_t file_base,
+                                 RecordColumnsDev cols, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_record_columns, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, u, offs, n, bstart, buoff,
+                     busize, nblocks, file_base, cols);
+  return hipGetLastError();
+}
+
+}  // namespace sbam

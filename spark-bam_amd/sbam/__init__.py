@@ -99,12 +99,23 @@ class _SplitArgs(ctypes.Structure):
                 ("use_success_bitmap", ctypes.c_int32)]
 
 
+class _RecordColumns(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("offset", "block_pos", "block_off", "block_size", "ref_id", "pos",
+                                               "bin_mq_nl", "flag_nc", "l_seq", "next_ref_id", "next_pos", "tlen")]
+
+
+RECORD_COLUMNS = {"offset": np.int64, "block_pos": np.int64, "block_off": np.int32, "block_size": np.int32,
+                  "ref_id": np.int32, "pos": np.int32, "bin_mq_nl": np.uint32, "flag_nc": np.uint32,
+                  "l_seq": np.int32, "next_ref_id": np.int32, "next_pos": np.int32, "tlen": np.int32}
+
+
 EXPORTS = [  # every symbol include/sbam.h declares
     "sbam_open", "sbam_close", "sbam_last_error", "sbam_reset", "sbam_version", "sbam_find_block_starts", "sbam_scan_blocks",
     "sbam_get_blocks", "sbam_inflate", "sbam_read_uncompressed", "sbam_pos_to_offset", "sbam_offset_to_pos",
     "sbam_header", "sbam_set_contig_lengths", "sbam_check_eager", "sbam_check_full_words", "sbam_check_full_counts",
     "sbam_find_record_start", "sbam_file_splits", "sbam_split_records", "sbam_compute_splits",
-    "sbam_record_offsets", "sbam_last_kernel_ms",
+    "sbam_record_offsets", "sbam_load_records", "sbam_get_record_columns", "sbam_record_columns_device",
+    "sbam_last_kernel_ms",
 ]
 
 _lib = None
@@ -142,6 +153,9 @@ def load_library(path: str = LIB_PATH):
         "sbam_split_records": (ctypes.c_int, [vp, P(_SplitArgs), i64, i64, vp, vp, vp]),
         "sbam_compute_splits": (ctypes.c_int, [vp, P(_SplitArgs), vp, i64, P(i64)]),
         "sbam_record_offsets": (ctypes.c_int, [vp, i64, i64, vp, i64, P(i64)]),
+        "sbam_load_records": (ctypes.c_int, [vp, P(_SplitArgs), i64, i64, vp, P(i64)]),
+        "sbam_get_record_columns": (ctypes.c_int, [vp, i64, i64, P(_RecordColumns)]),
+        "sbam_record_columns_device": (ctypes.c_int, [vp, P(_RecordColumns), P(i64)]),
         "sbam_last_kernel_ms": (ctypes.c_double, [vp, ctypes.c_char_p]),
     }
     for name, (res, args) in sig.items():
@@ -466,25 +480,48 @@ class BamFile:
         self._check(self.L.sbam_record_offsets(self.ctx, x0, x_end, _ptr(out), cap, ctypes.byref(n)))
         return out[: n.value]
 
+    def load_records(self, split_size: int, first: int = 0, count: Optional[int] = None,
+                     bgzf_blocks_to_check: int = BGZF_BLOCKS_TO_CHECK, reads_to_check: int = READS_TO_CHECK,
+                     max_read_size: int = MAX_READ_SIZE, use_success_bitmap: bool = False,
+                     columns: Optional[Sequence[str]] = tuple(RECORD_COLUMNS)):
+        """Records of Hadoop splits [first, first+count) decoded on the GPU (sbam_load_records): returns
+        (partition sizes, {column: ndarray}) with the records of all those splits concatenated in split order.
+        `columns=None` leaves the columns on the device (count only)."""
+        ns = len(hadoop_splits(self.file_size, split_size))
+        count = ns - first if count is None else count
+        sizes = np.zeros(max(count, 1), np.int64)
+        n = ctypes.c_int64(0)
+        a = self._args(split_size, bgzf_blocks_to_check, reads_to_check, max_read_size, use_success_bitmap)
+        self._check(self.L.sbam_load_records(self.ctx, ctypes.byref(a), first, count, _ptr(sizes), ctypes.byref(n)))
+        sizes = sizes[:count]
+        if columns is None:
+            return sizes, {}
+        cols = {k: np.zeros(n.value, RECORD_COLUMNS[k]) for k in columns}
+        rc = _RecordColumns(**{k: v.ctypes.data for k, v in cols.items()})
+        self._check(self.L.sbam_get_record_columns(self.ctx, 0, n.value, ctypes.byref(rc)))
+        return sizes, cols
+
     def load_reads_and_positions(self, split_size: int, **kw):
-        """loadReadsAndPositions: per partition, list of (Pos, record bytes) (CanLoadBam.scala:281-334)."""
-        st, cs, us, uo = self.blocks()
-        parts = []
-        for (start, end), (p0, nonempty, n) in zip(hadoop_splits(self.file_size, split_size),
-                                                   self.split_records(split_size, **kw)):
-            if not n:
-                parts.append([])
-                continue
-            x0 = self.offset_of(p0)
-            b = int(np.searchsorted(st, end, side="left"))
-            x_end = int(uo[b]) if b < st.size else self.uncompressed_size
-            offs = self.record_offsets(x0, x_end)
+        """loadReadsAndPositions: per partition, list of (Pos, record bytes) (CanLoadBam.scala:281-334).  Record
+        offsets and Pos come from sbam_load_records; each partition's bytes are one contiguous stream slice."""
+        sizes, c = self.load_records(split_size, columns=("offset", "block_pos", "block_off", "block_size"), **kw)
+        parts, i = [], 0
+        for n in sizes.tolist():
             recs = []
-            for o in offs.tolist():
-                bs = int.from_bytes(self.read_uncompressed(o, 4), "little", signed=True)
-                recs.append((self.pos_of(o), self.read_uncompressed(o, 4 + bs)))
+            if n:
+                off, bs = c["offset"][i:i + n], c["block_size"][i:i + n]
+                x0, x1 = int(off[0]), int(off[-1]) + 4 + int(bs[-1])
+                raw = self.read_uncompressed(x0, x1 - x0)
+                for j in range(n):
+                    o = int(off[j]) - x0
+                    recs.append((Pos(int(c["block_pos"][i + j]), int(c["block_off"][i + j])), raw[o:o + 4 + int(bs[j])]))
             parts.append(recs)
+            i += n
         return parts
+
+    def load_reads(self, split_size: int, **kw):
+        """sc.loadReads (CanLoadBam.scala:348-352): per partition, list of record bytes."""
+        return [[r for (_, r) in p] for p in self.load_reads_and_positions(split_size, **kw)]
 
 
 def read_name(record: bytes) -> str:

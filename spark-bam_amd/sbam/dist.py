@@ -108,6 +108,16 @@ def shard_pass(f, p: ShardPlan, split_size: int, R: int = 10) -> ShardResult:
                        n.astype(np.int64))
 
 
+def shard_load(f, p: ShardPlan, split_size: int, R: int = 10, use_success_bitmap: bool = False) -> np.ndarray:
+    """One shard's loadReads: the owned Hadoop splits' records decoded into device columns
+    (sbam_load_records; CanLoadBam.scala:281-334); returns the partition sizes."""
+    if not p.split_count:
+        return np.zeros(0, np.int64)
+    sizes, _ = f.load_records(split_size, first=p.split_first, count=p.split_count, reads_to_check=R,
+                              use_success_bitmap=use_success_bitmap, columns=None)
+    return sizes
+
+
 class GpuShard:
     """Per-rank GPU work for one shard: scan → inflate → full check (owned positions) → split records."""
 
@@ -133,15 +143,27 @@ class GpuShard:
         self.f.run(contig_lengths=self.contig_lengths)
         return shard_pass(self.f, self.plan, self.split_size, self.R)
 
-    def step(self) -> ShardResult:
+    def _retry(self, fn):
         while True:
             try:
-                return self._once()
+                return fn()
             except self.sbam.HaloException:
                 if self.plan.load_range(self.halo)[1] >= self.plan.file_size:
                     raise
                 self.halo *= 4
                 self._open()
+
+    def step(self) -> ShardResult:
+        """compute-splits + full-check of the shard."""
+        return self._retry(self._once)
+
+    def load_step(self) -> np.ndarray:
+        """loadReads of the shard: scan → inflate → FindBlockStart/FindRecordStart → record chains → columns."""
+        def once():
+            self.f.reset()
+            self.f.run(contig_lengths=self.contig_lengths)
+            return shard_load(self.f, self.plan, self.split_size, self.R)
+        return self._retry(once)
 
     def close(self):
         if self.f is not None:
