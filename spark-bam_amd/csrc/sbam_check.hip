@@ -331,9 +331,9 @@ SB_DEV uint32_t ref_bits_lds(int32_t ri, int32_t rp, const int32_t *lensL, int32
 // Record 0 at x (full.Checker.scala:22-184 / eager.Checker.scala:24-126 for k = 0), fixed fields in f[],
 // rel = x - tile base.  Every check is evaluated unconditionally from the tile (clamped LDS reads, no
 // per-lane branches) so a wave's lanes cost the same; only the rare tails (a name body or an op array
-// running past 64 checked bytes / ops) branch out to HBM.  INTERIOR: the tile ends at least kInteriorTail
-// bytes before the stream end, so no read of record 0 (36 fixed bytes, <= 255 name bytes, <= 65535 ops) can
-// reach EOF and the EOF arithmetic drops out.
+// running past 64 checked bytes / ops) branch out to HBM.  INTERIOR: the tile lies inside [x0, x1) and ends at
+// least kInteriorTail bytes before the stream end, so no read of record 0 (36 fixed bytes, <= 255 name bytes,
+// <= 65535 ops) can reach EOF: the EOF arithmetic and the range checks drop out.
 constexpr int64_t kInteriorTail = 262144 + 512;
 template <bool EAGER, bool INTERIOR>
 SB_DEV uint32_t check_first(const Tile &t, const StreamView &sv, const int32_t *lensL, int64_t x, int rel, int R,
@@ -435,10 +435,12 @@ struct Planes {  // carry-save bit planes: per-flag counts of up to 255 values p
 // Count one checked position into the lane's accumulators (full-check Counts semantics).
 struct Acc {
   Planes pl;
+  Planes kp;         // interior tiles: one-hot key planes (bit k = a position with key k; bit 0 = PASS0, ignored)
   uint64_t keyc[3];  // 8-bit counters per key (8 per word)
   uint32_t n_succ, n_tff, n_halo;
   SB_DEV void clear() {
     pl.clear();
+    kp.clear();
     keyc[0] = keyc[1] = keyc[2] = 0;
     n_succ = n_tff = n_halo = 0;
   }
@@ -480,6 +482,32 @@ struct Acc {
   }
 };
 
+// Record-0 pass over an interior tile (every position in [x0, x1), no EOF in reach): a result is either PASS0
+// (flag bits 0) or a failure with k = 0, never Success / HALO / TooFewFixedBlockBytes.  So F = w & 0x7ffff,
+// key = popc(F), and the key histogram is a one-hot word added into bit planes like the flags (no per-key
+// selects).  Only keys 1-2 take the rare per-flag / pair path.
+SB_DEV uint32_t classify_interior(uint32_t w, uint32_t *k12, uint32_t *pair, uint32_t &onehot) {
+  const uint32_t F = w & 0x7ffffu;
+  const uint32_t key = (uint32_t)__popc(F);
+  onehot = 1u << key;
+  if (F && key <= 2) {
+    for (uint32_t m = F; m; m &= m - 1) atomicAdd(&k12[key * 19 + __builtin_ctz(m)], 1u);
+    if (key == 2) {
+      const uint32_t fi = __builtin_ctz(F), rest = F & (F - 1);
+      atomicAdd(&pair[fi * 19 + (rest ? __builtin_ctz(rest) : fi)], 1u);
+    }
+  }
+  return F;
+}
+
+// 4:3 compressor of four bit-plane words into (ones, twos, fours) for Planes::add
+SB_DEV void add4(Planes &pl, const uint32_t v[4]) {
+  const uint32_t x1a = v[0] ^ v[1], c1 = v[0] & v[1];
+  const uint32_t x2a = v[2] ^ v[3], c2 = v[2] & v[3];
+  const uint32_t ones = x1a ^ x2a, c3 = x1a & x2a;
+  pl.add(ones, c1 ^ c2 ^ c3, (c1 & c2) | (c3 & (c1 ^ c2)));
+}
+
 // Reduce the lanes' accumulators into the workgroup's LDS totals (ballots over bit planes; wave sums).
 SB_DEV void flush_acc(Acc &acc, unsigned long long *s_acc, int lane) {
 #pragma unroll
@@ -491,7 +519,11 @@ SB_DEV void flush_acc(Acc &acc, unsigned long long *s_acc, int lane) {
   }
 #pragma unroll
   for (int k = 0; k < 21; k++) {
-    const uint32_t v = wave_sum((uint32_t)(acc.keyc[k >> 3] >> (8 * (k & 7))) & 0xffu);
+    uint32_t v = wave_sum((uint32_t)(acc.keyc[k >> 3] >> (8 * (k & 7))) & 0xffu);
+    if (k >= 1 && k <= 19) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) v += (uint32_t)__popcll(__ballot((acc.kp.p[j] >> k) & 1u)) << j;
+    }
     if (lane == 0 && v) atomicAdd(&s_acc[19 + k], (unsigned long long)v);
   }
   const uint32_t a = wave_sum(acc.n_succ), b = wave_sum(acc.n_tff), h = wave_sum(acc.n_halo);
@@ -603,7 +635,7 @@ __global__ __launch_bounds__(kCheckThreads, 4) void k_check(StreamView sv, int64
 #pragma unroll
         for (int q = 0; q < 8; q++) f[q] = (int32_t)__builtin_amdgcn_alignbyte(W[q + 1], W[q], o);
         uint32_t w = check_first<EAGER, INTERIOR>(tl, sv, lensL, x, 4 * g + o, R, f);
-        w = (x >= x0 && x < x1) ? w : W_NONE;
+        if (!INTERIOR) w = (x >= x0 && x < x1) ? w : W_NONE;  // interior tiles lie inside [x0, x1)
         wd[o] = w;
       }
       if (MODE == MODE_WORDS) {
@@ -620,28 +652,33 @@ __global__ __launch_bounds__(kCheckThreads, 4) void k_check(StreamView sv, int64
       v |= shfl_xor64(v, 2);
       v |= shfl_xor64(v, 4);
       v |= shfl_xor64(v, 8);
-      if ((lane & 15) == 0 && xg < x1) bitmap[(xg - x0a) >> 6] = v;  // word holds >= 1 position < x1
+      if ((lane & 15) == 0 && (INTERIOR || xg < x1)) bitmap[(xg - x0a) >> 6] = v;  // word holds >= 1 position < x1
       if (!COUNTS) continue;
 #if SBAM_ABLATE == 3  // timing experiment only: no counting
       continue;
 #endif
       uint32_t Fo[4];
+      if constexpr (INTERIOR && !BYKEY) {
+        uint32_t oh[4];
 #pragma unroll
-      for (int o = 0; o < 4; o++) {
-        uint32_t key = 0;
-        bool counted = false;
-        Fo[o] = 0;
-        if (wd[o] != W_NONE && wd[o] != W_PASS0)
-          Fo[o] = acc.classify<BYKEY>(wd[o], cd, s_k12, s_pair, key, counted);
-        if (BYKEY) bykey_count(s_cnt, lane, counted, key, Fo[o]);
+        for (int o = 0; o < 4; o++) Fo[o] = classify_interior(wd[o], s_k12, s_pair, oh[o]);
+        add4(acc.kp, oh);
+      } else {
+#pragma unroll
+        for (int o = 0; o < 4; o++) {
+          uint32_t key = 0;
+          bool counted = false;
+          Fo[o] = 0;
+          if (wd[o] != W_NONE && wd[o] != W_PASS0)
+            Fo[o] = acc.classify<BYKEY>(wd[o], cd, s_k12, s_pair, key, counted);
+          if (BYKEY) bykey_count(s_cnt, lane, counted, key, Fo[o]);
+        }
       }
-      const uint32_t x1a = Fo[0] ^ Fo[1], c1 = Fo[0] & Fo[1];
-      const uint32_t x2a = Fo[2] ^ Fo[3], c2 = Fo[2] & Fo[3];
-      const uint32_t ones = x1a ^ x2a, c3 = x1a & x2a;
-      acc.pl.add(ones, c1 ^ c2 ^ c3, (c1 & c2) | (c3 & (c1 ^ c2)));
+      add4(acc.pl, Fo);
     }
     };
-    if (base + kTile + kInteriorTail <= sv.L) run_tile(std::integral_constant<bool, true>{});
+    if (base >= x0 && base + kTile <= x1 && base + kTile + kInteriorTail <= sv.L)
+      run_tile(std::integral_constant<bool, true>{});
     else run_tile(std::integral_constant<bool, false>{});
     if (COUNTS) {
       if (++since_flush == kFlushTiles) {
