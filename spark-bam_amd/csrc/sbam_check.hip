@@ -242,31 +242,78 @@ SB_DEV void count_chain_result(const CountsDev &cd, uint32_t w, bool bykey) {
   if (kk > 0) atomicAdd(&cd.rbe[key * 128 + kk], 1ull);
 }
 
-// One lane per bitmap word; cd.counts == nullptr skips counting (eager), words != nullptr writes results.
+// One workgroup per chunk of kChainWords bitmap words: the chunk's PASS0 positions are compacted into an LDS
+// list (popcount + workgroup scan) and the 256 threads walk the listed chains, a chain per thread, so every lane of
+// a wave does the same R hops.  (Walking the set bits of one word per lane made each wave pay the busiest
+// lane's chains: 15 ms at 10 GB, for ~0.2 chains per word.)  cd.counts == nullptr skips counting (eager);
+// words != nullptr writes results.  A failing chain clears its bit with an atomic AND (other threads of the
+// workgroup may clear bits of the same word); each thread keeps its words as first read, so the list of a
+// chunk with more than kChainList chains stays the same across rounds while bits are being cleared.
+constexpr int kChainWordsPerThread = 8;
+constexpr int kChainWords = 256 * kChainWordsPerThread;  // 131 072 positions per chunk
+constexpr int kChainList = 4096;                          // LDS list entries per round (chunk-relative u32)
 __global__ __launch_bounds__(256) void k_chains(StreamView sv, int64_t x0, int64_t x1, int R,
                                                 unsigned long long *__restrict__ bitmap, CountsDev cd, int bykey,
                                                 uint32_t *__restrict__ words) {
+  __shared__ uint32_t s_list[kChainList];
+  __shared__ uint32_t s_wsum[4];
   const int64_t x0a = x0 & ~(int64_t)63;
   const int64_t nwords = (x1 - x0a + 63) >> 6;
+  const int64_t nchunks = (nwords + kChainWords - 1) / kChainWords;
+  const int tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
   uint32_t n_succ = 0;
-  for (int64_t wi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; wi < nwords; wi += (int64_t)gridDim.x * blockDim.x) {
-    const unsigned long long m = bitmap[wi];
-    if (!m) continue;
-    unsigned long long keep = m;
-    for (unsigned long long q = m; q; q &= q - 1) {
-      const int b = __builtin_ctzll(q);
-      const int64_t p = x0a + 64 * wi + b;
-      const uint32_t w = walk_chain(sv, bitmap, x0a, x1, p, R);
-      if (w & W_SUCC) n_succ++;
-      else keep &= ~(1ull << b);
-      if (cd.counts) count_chain_result(cd, w, bykey != 0);
-      if (words) words[p - x0] = w;
+  for (int64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const int64_t w0 = ch * kChainWords + (int64_t)tid * kChainWordsPerThread;
+    unsigned long long cw[kChainWordsPerThread];
+    uint32_t mine = 0;
+#pragma unroll
+    for (int j = 0; j < kChainWordsPerThread; j++) {
+      cw[j] = w0 + j < nwords ? bitmap[w0 + j] : 0ull;
+      mine += (uint32_t)__popcll(cw[j]);
     }
-    if (keep != m) bitmap[wi] = keep;
+    // workgroup exclusive scan of the per-thread counts
+    uint32_t incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    __syncthreads();  // s_wsum / s_list of the previous chunk are no longer read
+    if (lane == 63) s_wsum[wv] = incl;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      before += k < wv ? s_wsum[k] : 0u;
+      total += s_wsum[k];
+    }
+    const uint32_t first = before + incl - mine;
+    const int64_t cbase = x0a + ch * (int64_t)kChainWords * 64;
+    for (uint32_t r0 = 0; r0 < total; r0 += kChainList) {
+      if (mine && first < r0 + kChainList && first + mine > r0) {
+        uint32_t idx = first;
+#pragma unroll
+        for (int j = 0; j < kChainWordsPerThread; j++) {
+          for (unsigned long long m = cw[j]; m && idx < r0 + kChainList; m &= m - 1, idx++)
+            if (idx >= r0) s_list[idx - r0] = (uint32_t)(((w0 + j) << 6) + __builtin_ctzll(m) - (cbase - x0a));
+        }
+      }
+      __syncthreads();
+      const uint32_t n = min((uint32_t)kChainList, total - r0);
+      for (uint32_t i = tid; i < n; i += 256) {
+        const int64_t p = cbase + s_list[i];
+        const uint32_t w = walk_chain(sv, bitmap, x0a, x1, p, R);
+        if (w & W_SUCC) n_succ++;
+        else atomicAnd(&bitmap[(p - x0a) >> 6], ~(1ull << ((p - x0a) & 63)));
+        if (cd.counts) count_chain_result(cd, w, bykey != 0);
+        if (words) words[p - x0] = w;
+      }
+      __syncthreads();
+    }
   }
   if (cd.counts) {
     for (int o = 32; o >= 1; o >>= 1) n_succ += __shfl_xor((int)n_succ, o, 64);
-    if (lane_id() == 0 && n_succ) atomicAdd(&cd.scalars[1], (unsigned long long)n_succ);
+    if (lane == 0 && n_succ) atomicAdd(&cd.scalars[1], (unsigned long long)n_succ);
   }
 }
 
@@ -801,8 +848,8 @@ static int check_grid(int64_t ntiles) { return (int)(ntiles < 1 ? 1 : ntiles > 2
 static int64_t ntiles_of(int64_t x0, int64_t x1) { return (x1 - (x0 & ~(int64_t)63) + kTile - 1) / kTile; }
 static int chain_grid(int64_t x0, int64_t x1) {
   const int64_t words = (x1 - (x0 & ~(int64_t)63) + 63) >> 6;
-  const int64_t g = (words + 255) / 256;
-  return (int)(g < 1 ? 1 : g > 8192 ? 8192 : g);
+  const int64_t g = (words + kChainWords - 1) / kChainWords;
+  return (int)(g < 1 ? 1 : g > 65535 ? 65535 : g);
 }
 
 hipError_t launch_check_full_counts(StreamView sv, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,

@@ -1,0 +1,380 @@
+"""spark-bam CLI drop-ins over the GPU path: `full-check`, `compute-splits -s`, `count-reads`.
+
+    python -m sbam.cli full-check [-l LIMIT] [-m SPLIT] [-i RANGES] [-r READS] BAM [OUT]
+    python -m sbam.cli compute-splits [-s] [-l LIMIT] [-m SPLIT] BAM [OUT]
+    python -m sbam.cli count-reads [-m SPLIT] BAM [OUT]
+
+Report text follows the reference apps line for line, so the goldens of cli/src/test/resources/output/ diff
+verbatim (tests/test_cli.py):
+  * full-check: FullCheck.scala:141-322, the CheckerApp summary (CheckerApp.scala:140-222) when a `.records`
+    sidecar is present, PosMetadata / NextRecord (check/PosMetadata.scala, NextRecord.scala), Counts.lines
+    (check/.../full/error/Counts.scala:59-127);
+  * compute-splits: ComputeSplits.scala:56-68 (-s: spark-bam splits only; hadoop-bam comparison is out of scope);
+  * count-reads: compare/CountReads.scala:80-100, spark-bam side only.
+Counting, checking and splitting all run through libsbam.so (sbam.BamFile); this module only formats."""
+from __future__ import annotations
+
+import argparse
+import math
+import os
+import sys
+import time
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+import sbam
+from sbam import FLAG_NAMES, Pos
+
+RATIO = 3.0  # EstimatedCompressionRatio default (bgzf/.../EstimatedCompressionRatio.scala)
+
+
+# ---- small formatting helpers ----------------------------------------------------------------------------
+def parse_bytes(s: str) -> int:
+    """hammerlab Bytes arguments: 230k, 2m, 1g (binary multiples), or a plain byte count."""
+    s = s.strip().lower()
+    mult = {"k": 1 << 10, "m": 1 << 20, "g": 1 << 30, "t": 1 << 40}
+    if s and s[-1] == "b":
+        s = s[:-1]
+    if s and s[-1] in mult:
+        return int(float(s[:-1]) * mult[s[-1]])
+    return int(s)
+
+
+def format_bytes(n: int) -> str:
+    """Bytes.format as the goldens show it: three significant digits of the binary unit (25.6K, 217K, 583K)."""
+    units = "KMGTPE"
+    if n < 1024:
+        return f"{n}B"
+    v, u = float(n), -1
+    while v >= 1024 and u < len(units) - 1:
+        v /= 1024
+        u += 1
+    s = f"{v:.0f}" if v >= 100 else f"{v:.1f}" if v >= 10 else f"{v:.2f}"
+    return s + units[u]
+
+
+def parse_ranges(s: str) -> List[Tuple[int, int]]:
+    """-i ranges of compressed block starts: `0`, `26169`, `0-200k`, comma-separated ([lo, hi) each; a single
+    value N is the point range [N, N+1))."""
+    out = []
+    for part in s.split(","):
+        part = part.strip()
+        if "-" in part:
+            a, b = part.split("-", 1)
+            out.append((parse_bytes(a), parse_bytes(b)))
+        else:
+            v = parse_bytes(part)
+            out.append((v, v + 1))
+    return out
+
+
+def show_flags(F: int) -> str:
+    return ",".join(FLAG_NAMES[i] for i in range(19) if F >> i & 1)
+
+
+def count_lines(pairs: Sequence[Tuple[str, int]], include_zeros: bool, hide_tff: bool,
+                reads_before_error: Optional[Sequence[Tuple[int, int]]] = None) -> List[str]:
+    """Counts.lines (Counts.scala:80-127): fields sorted by value, descending, ties in field order (stable)."""
+    rows = [(k, str(v)) for k, v in sorted(pairs, key=lambda kv: -kv[1])
+            if (v > 0 or include_zeros) and (k != "tooFewFixedBlockBytes" or not hide_tff)]
+    if reads_before_error:
+        rows.append(("readsBeforeError", " ".join(f"{r}ⅹ{n}" for r, n in sorted(reads_before_error))))
+    if not rows:
+        return []
+    mk = max(len(k) for k, _ in rows)
+    mv = max(len(v) for _, v in rows)
+    return [f"{' ' * (mk - len(k))}{k}:\t{' ' * (mv - len(v))}{v}" for k, v in rows]
+
+
+def print_limited(out: List[str], items: Sequence[str], total: Optional[int], header: str, trunc_header,
+                  limit: int, indent: str = ""):
+    """hammerlab cli `print(...)`: header, then at most `limit` indented items and `…` when truncated."""
+    n_total = len(items) if total is None else total
+    if n_total > limit:
+        out.append(indent + trunc_header(limit))
+        out.extend(indent + "\t" + x for x in items[:limit])
+        out.append(indent + "\t…")
+    else:
+        out.append(indent + header)
+        out.extend(indent + "\t" + x for x in items)
+
+
+# ---- record display (PosMetadata.showRecord over htsjdk SAMRecord.toString) -------------------------------
+def show_record(rec: bytes, contig_names: Sequence[str]) -> str:
+    ref = int.from_bytes(rec[4:8], "little", signed=True)
+    pos = int.from_bytes(rec[8:12], "little", signed=True)
+    lrn = rec[12]
+    flag = int.from_bytes(rec[18:20], "little")
+    l_seq = int.from_bytes(rec[20:24], "little", signed=True)
+    name = rec[36:36 + max(lrn - 1, 0)].decode("latin-1")
+    s = name
+    if flag & 1:
+        s += " 1/2" if flag & 0x40 else " 2/2"
+    s += f" {l_seq}b"
+    unmapped = bool(flag & 4)
+    s += " unmapped read" if unmapped else " aligned read"  # SAMRecord.toString minus its trailing '.'
+    start = pos + 1  # getStart: 1-based alignment start
+    where = f"{contig_names[ref] if 0 <= ref < len(contig_names) else ref}:{start}"
+    if unmapped and start >= 0 and 0 <= ref < len(contig_names):
+        s += f" (placed at {where})"
+    elif not unmapped:
+        s += f" @ {where}"
+    return s
+
+
+# ---- full-check ----------------------------------------------------------------------------------------------
+class FullCheckReport:
+    """full-check over the blocks selected by `ranges` (None = whole file)."""
+
+    def __init__(self, f: sbam.BamFile, data: bytes, records_path: Optional[str], limit: int = 10,
+                 ranges: Optional[List[Tuple[int, int]]] = None, reads_to_check: int = 10):
+        self.f, self.data, self.limit, self.R = f, data, limit, reads_to_check
+        st, cs, us, uo = f.blocks()
+        sel = np.ones(st.size, bool) if ranges is None else \
+            np.any([(st >= lo) & (st < hi) for lo, hi in ranges], axis=0)
+        self.runs = self._runs(np.nonzero(sel)[0], uo, us)
+        self.compressed = int(cs[sel].astype(np.int64).sum())
+        self.records_path = records_path
+        self.names = header_names(f)
+
+    @staticmethod
+    def _runs(idx, uo, us):
+        """contiguous block-index runs → uncompressed [x0, x1) ranges"""
+        runs = []
+        for b in idx.tolist():
+            x0, x1 = int(uo[b]), int(uo[b]) + int(us[b])
+            if runs and runs[-1][1] == x0:
+                runs[-1][1] = x1
+            else:
+                runs.append([x0, x1])
+        return [(a, b) for a, b in runs]
+
+    def close_calls(self, key: int, want: int) -> List[Tuple[int, int]]:
+        """First `want` positions (file order) whose result has exactly `key` non-zero fields."""
+        got = []
+        chunk = 1 << 24
+        for x0, x1 in self.runs:
+            for a in range(x0, x1, chunk):
+                b = min(x1, a + chunk)
+                w = self.f.check_full_words(a, b, self.R)
+                F = (w & 0x7ffff).astype(np.uint32)
+                kk = (w >> 24) & 0x7f
+                pop = np.zeros(F.size, np.int64)
+                for i in range(19):
+                    pop += (F >> i) & 1
+                counted = ((w & 0x80000000) == 0) & ~((F == 1) & (kk == 0))
+                hit = np.nonzero(counted & (pop + (kk > 0) == key))[0]
+                for h in hit[: want - len(got)].tolist():
+                    got.append((a + h, int(w[h])))
+                if len(got) >= want:
+                    return got
+        return got
+
+    def pos_metadata(self, x: int, w: int) -> str:
+        p = self.f.pos_of(x)
+        nxt = self.next_record(x)
+        if nxt is None:
+            desc = "no next record"
+        else:
+            y, delta = nxt
+            bs = int.from_bytes(self.f.read_uncompressed(y, 4), "little", signed=True)
+            desc = f"{delta} before {show_record(self.f.read_uncompressed(y, 4 + bs), self.names)}"
+        return f"{p}:\t{desc}. Failing checks: {show_flags(w & 0x7ffff)}"
+
+    def next_record(self, x: int, max_read_size: int = 10_000_000):
+        """FindRecordStart.withDelta(pos) (FindRecordStart.scala:30-63): first eager-true offset >= x."""
+        L = self.f.uncompressed_size
+        lim = min(L, x + max_read_size)
+        a, step = x, 1 << 20
+        while a < lim:
+            b = min(lim, a + step)
+            calls = self.f.check_eager(a, b, self.R)
+            hit = np.nonzero(calls)[0]
+            if hit.size:
+                return a + int(hit[0]), a + int(hit[0]) - x
+            a = b
+        return None
+
+    def lines(self) -> List[str]:
+        f, out = self.f, []
+        counts = None
+        c_by_key = np.zeros((21, 19), np.int64)
+        npos = np.zeros(21, np.int64)
+        totals = np.zeros(19, np.int64)
+        rbe = np.zeros((21, 128), np.int64)
+        pair = np.zeros((19, 19), np.int64)
+        n_positions = n_success = 0
+        calls_bits = []
+        for x0, x1 in self.runs:
+            c, bits = f.check_full_counts(x0, x1, self.R, want_bitmap=True, by_key=True)
+            c_by_key += c.by_key
+            npos += c.positions
+            totals += c.totals
+            rbe += c.reads_before_error
+            pair += c.pair_hist
+            n_positions += x1 - x0
+            n_success += c.n_success
+            calls_bits.append((x0, bits))
+        if self.records_path and os.path.exists(self.records_path):
+            truth = set()
+            for line in open(self.records_path):
+                if line.strip():
+                    b, o = (int(v) for v in line.split(","))
+                    truth.add(f.offset_of(Pos(b, o)))
+            tp = fp = fn = 0
+            for x0, bits in calls_bits:
+                called = set((x0 + np.nonzero(bits)[0]).tolist())
+                expected = {t for t in truth if x0 <= t < x0 + bits.size}
+                tp += len(called & expected)
+                fp += len(called - expected)
+                fn += len(expected - called)
+            if fp or fn:  # FullCheck.scala:108-114: a mismatch is an error
+                raise RuntimeError(f"{fp} false positives, {fn} false negatives against {self.records_path}")
+            ratio = n_positions / self.compressed if self.compressed else float("nan")
+            out += [f"{n_positions} uncompressed positions", f"{format_bytes(self.compressed)} compressed",
+                    "Compression ratio: %.2f" % ratio, f"{tp + fn} reads", "All calls matched!", ""]
+        field_names = FLAG_NAMES[:19]
+
+        def pairs(vec):
+            return [(field_names[i], int(vec[i])) for i in range(19)]
+
+        if npos[1] > 0:  # critical (key-1) section, FullCheck.scala:230-258
+            out.append("Critical error counts (true negatives where only one check failed):")
+            out += ["\t" + l for l in count_lines(pairs(c_by_key[1]), False, False)]
+            out.append("")
+            n1 = int(npos[1])
+            items = [self.pos_metadata(x, w) for x, w in self.close_calls(1, self.limit)]
+            print_limited(out, items, n1, f"{n1} critical positions:",
+                          lambda n: f"{n} of {n1} critical positions:", self.limit)
+        else:
+            out.append("No positions where only one check failed")
+        out.append("")
+        if npos[2] > 0:  # close calls (key 2), FullCheck.scala:262-306
+            n2 = int(npos[2])
+            items = [self.pos_metadata(x, w) for x, w in self.close_calls(2, self.limit)]
+            print_limited(out, items, n2, f"{n2} positions where exactly two checks failed:",
+                          lambda n: f"{n} of {n2} positions where exactly two checks failed:", self.limit)
+            out.append("")
+            hist = []
+            for i in range(19):
+                for j in range(19):
+                    if pair[i, j]:
+                        F = (1 << i) | (1 << j)
+                        hist.append((int(pair[i, j]), F))
+            hist.sort(key=lambda t: -t[0])  # stable: reduceByKey output order is not pinned beyond the counts
+            if hist and hist[0][0] > 1:
+                print_limited(out, [f"{n}:\t{show_flags(F)}" for n, F in hist], None, "Histogram:",
+                              lambda _: "Histogram:", self.limit, indent="\t")
+                out.append("")
+            out.append("\tPer-flag totals:")
+            out += ["\t\t" + l for l in count_lines(pairs(c_by_key[2]), False, False)]
+            out.append("")
+        else:
+            out += ["No positions where exactly two checks failed", ""]
+        rb = [(k, int(rbe[:, k].sum())) for k in range(1, 128) if rbe[:, k].sum()]
+        out.append("Total error counts:")
+        out += ["\t" + l for l in count_lines(pairs(totals), True, True, rb)]
+        out.append("")
+        return out
+
+
+def header_names(f: sbam.BamFile) -> List[str]:
+    """Contig names from the BAM header in the device stream (check/.../bam/header/Header.scala:26-60)."""
+    u = f.read_uncompressed(0, min(f.uncompressed_size, 1 << 20))
+    if u[:4] != b"BAM\x01":
+        return []
+    lt = int.from_bytes(u[4:8], "little")
+    p = 8 + lt
+    n = int.from_bytes(u[p:p + 4], "little")
+    p += 4
+    names = []
+    for _ in range(n):
+        ln = int.from_bytes(u[p:p + 4], "little")
+        names.append(u[p + 4:p + 4 + ln - 1].decode("latin-1"))
+        p += 4 + ln + 4
+    return names
+
+
+# ---- compute-splits / count-reads ------------------------------------------------------------------------
+def split_length(s: sbam.Split) -> int:
+    """Split.length = Pos.-(end, start) (bgzf/.../Pos.scala:17-22), then .toInt in ComputeSplits."""
+    return int(max(0, s.end.block_pos - s.start.block_pos + math.trunc((s.end.offset - s.start.offset) / RATIO)))
+
+
+def _num(v: float) -> str:
+    r = round(v, 1)
+    return str(int(r)) if r == int(r) else f"{r:.1f}"
+
+
+def stats_lines(xs: Sequence[int]) -> List[str]:
+    """hammerlab Stats for a small sample (the form ComputeSplitsTest pins): N, mean/population σ,
+    median/MAD, elements and sorted elements.  (Stats' histogram form for large N is not pinned by any
+    reference fixture.)"""
+    a = np.asarray(xs, np.float64)
+    n = a.size
+    if n == 0:
+        return ["N: 0"]
+    mean = a.mean()
+    sd = math.sqrt(((a - mean) ** 2).mean())
+    med = float(np.median(a))
+    mad = float(np.median(np.abs(a - med)))
+    return [f"N: {n}, μ/σ: {_num(mean)}/{_num(sd)}, med/mad: {_num(med)}/{_num(mad)}",
+            " elems: " + " ".join(str(int(v)) for v in xs),
+            "sorted: " + " ".join(str(int(v)) for v in sorted(xs))]
+
+
+def compute_splits_lines(f: sbam.BamFile, split_size: int, limit: int) -> List[str]:
+    t = time.perf_counter()
+    splits = f.compute_splits(split_size)
+    ms = int((time.perf_counter() - t) * 1e3)
+    out = [f"Get spark-bam splits: {ms}ms", "", "Split-size distribution:"]
+    out += stats_lines([split_length(s) for s in splits])
+    out.append("")
+    items = [str(s) for s in splits]
+    print_limited(out, items, None, f"{len(splits)} splits:", lambda n: f"First {n} of {len(splits)} splits:", limit)
+    out.append("")
+    return out
+
+
+def count_reads_lines(f: sbam.BamFile, split_size: int) -> List[str]:
+    t = time.perf_counter()
+    n = sum(f.partition_sizes(split_size))
+    ms = int((time.perf_counter() - t) * 1e3)
+    return [f"spark-bam read-count time: {ms}", "", f"spark-bam found {n} reads", ""]
+
+
+def main(argv: Optional[Sequence[str]] = None) -> int:
+    ap = argparse.ArgumentParser(prog="sbam.cli")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    for name in ("full-check", "compute-splits", "count-reads"):
+        p = sub.add_parser(name)
+        p.add_argument("-l", "--print-limit", type=int, default=10)
+        p.add_argument("-m", "--max-split-size", type=parse_bytes, default=2 << 20)
+        p.add_argument("bam")
+        p.add_argument("out", nargs="?")
+        if name == "full-check":
+            p.add_argument("-i", "--intervals", type=parse_ranges, default=None)
+            p.add_argument("-r", "--reads-to-check", type=int, default=10)
+        if name == "compute-splits":
+            p.add_argument("-s", "--spark-bam", action="store_true")
+    a = ap.parse_args(argv)
+    data = open(a.bam, "rb").read()
+    with sbam.BamFile(data, path=a.bam) as f:
+        if a.cmd == "full-check":
+            rep = FullCheckReport(f, data, a.bam + ".records", a.print_limit, a.intervals, a.reads_to_check)
+            lines = rep.lines()
+        elif a.cmd == "compute-splits":
+            lines = compute_splits_lines(f, a.max_split_size, a.print_limit)
+        else:
+            lines = count_reads_lines(f, a.max_split_size)
+    text = "\n".join(lines) + "\n"
+    if a.out:
+        open(a.out, "w").write(text)
+    else:
+        sys.stdout.write(text)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,142 @@
+"""CLI drop-ins (sbam.cli) against the reference's golden outputs, verbatim.
+
+full-check: cli/src/test/resources/output/full-check/* with the arguments of FullCheckTest.scala:12-68 (all
+`-l 10`).  compute-splits -s: the lines ComputeSplitsTest.scala:14-30 pins (the timing line is matched by
+shape, as the reference's `l"... ${d}ms"` matcher does).  The formatting helpers are checked on CPU; the
+report runs need libsbam.so on a GPU."""
+import os
+import re
+import shutil
+
+import pytest
+
+from conftest import FIXTURES, GOLDEN
+
+
+def test_format_bytes_and_sizes():
+    from sbam.cli import format_bytes, parse_bytes, parse_ranges
+    assert [format_bytes(n) for n in (597454, 531725, 221910, 26169, 24080)] == \
+        ["583K", "519K", "217K", "25.6K", "23.5K"]
+    assert parse_bytes("230k") == 230 * 1024 and parse_bytes("2m") == 2 << 20 and parse_bytes("100") == 100
+    assert parse_ranges("0-200k") == [(0, 204800)] and parse_ranges("26169") == [(26169, 26170)]
+
+
+def test_stats_lines_compute_splits_test():
+    # ComputeSplitsTest.scala:18-22 ("eager 230KB") and :73-77 ("compare 240KB")
+    from sbam.cli import stats_lines
+    assert stats_lines([224301, 244822, 113078]) == [
+        "N: 3, μ/σ: 194067/57877.4, med/mad: 224301/20521",
+        " elems: 224301 244822 113078",
+        "sorted: 113078 224301 244822"]
+    assert stats_lines([248438, 244941, 88822])[0] == "N: 3, μ/σ: 194067/74433.1, med/mad: 244941/3497"
+    assert stats_lines([242083, 253302, 134922])[0] == "N: 3, μ/σ: 210102.3/53357.5, med/mad: 242083/11219"
+
+
+def test_split_length():
+    from sbam import Pos, Split
+    from sbam.cli import split_length
+    assert split_length(Split(Pos(0, 45846), Pos(239479, 312))) == 224301
+    assert split_length(Split(Pos(239479, 312), Pos(484396, 25))) == 244822
+
+
+class OracleBam:
+    """sbam.BamFile-shaped view of a file on the CPU oracle: runs the report logic without a GPU (test
+    backend only; the CLI itself always opens libsbam.so)."""
+
+    def __init__(self, data):
+        import oracle
+        self.o = oracle.BamFile(data)
+        self.uncompressed_size = self.o.L
+
+    def blocks(self):
+        return self.o.start, self.o.csize, self.o.usize, self.o.uoff[:-1]
+
+    def check_full_counts(self, x0, x1, R=10, want_bitmap=False, by_key=False):
+        import numpy as np
+        import sbam
+        from test_gpu_parity import pair_hist
+        c, npos, rbe, ns = self.o.counts_range(x0, x1, R)
+        w = self.o.check_full_range(x0, x1, R)
+        C = sbam.Counts(c.sum(0), c, npos, rbe, pair_hist(w), x1 - x0, ns, int(np.sum(w == 1)))
+        return (C, (w & 0x80000000) != 0) if want_bitmap else C
+
+    def check_full_words(self, x0, x1, R=10):
+        return self.o.check_full_range(x0, x1, R)
+
+    def check_eager(self, x0, x1, R=10):
+        return (self.o.check_full_range(x0, x1, R) & 0x80000000) != 0
+
+    def read_uncompressed(self, x, n):
+        return self.o.u[x:x + n].tobytes()
+
+    def pos_of(self, x):
+        import sbam
+        p = self.o.pos_of(x)
+        return sbam.Pos(p.block_pos, p.offset)
+
+    def offset_of(self, p):
+        return self.o.offset_of(p)
+
+
+CASES = [
+    ("1.bam", "1.bam", ["-m", "200k"]),
+    ("1.noblocks.bam", "1.bam", ["-m", "200k"]),
+    ("2.bam.first", "2.bam", ["-i", "0"]),
+    ("2.bam.second", "2.bam", ["-i", "26169"]),
+    ("2.bam.200k", "2.bam", ["-i", "0-200k", "-m", "100k"]),
+    ("2.bam", "2.bam", []),
+]
+
+
+@pytest.mark.parametrize("golden,bam,args", CASES)
+def test_full_check_report_logic(golden, bam, args):
+    """The report assembly on the oracle backend reproduces every full-check golden verbatim."""
+    from sbam import cli
+    data = open(os.path.join(FIXTURES, bam), "rb").read()
+    ranges = cli.parse_ranges(args[args.index("-i") + 1]) if "-i" in args else None
+    records = os.path.join(FIXTURES, bam + ".records") if golden != "1.noblocks.bam" else None
+    rep = cli.FullCheckReport(OracleBam(data), data, records, 10, ranges)
+    assert "\n".join(rep.lines()) + "\n" == open(os.path.join(GOLDEN, "full-check", golden)).read()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("golden,bam,args", CASES)
+def test_full_check_report(golden, bam, args, tmp_path):
+    from sbam import cli
+    src = os.path.join(FIXTURES, bam)
+    path = tmp_path / bam
+    shutil.copy(src, path)
+    if golden != "1.noblocks.bam":  # bam1Unindexed: the same file without its .records / .blocks sidecars
+        shutil.copy(src + ".records", str(path) + ".records")
+    out = tmp_path / "out.txt"
+    assert cli.main(["full-check", "-l", "10", *args, str(path), str(out)]) == 0
+    want = open(os.path.join(GOLDEN, "full-check", golden)).read()
+    assert out.read_text() == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,split_lines,stats", [
+    ("230k", ["0:45846-239479:312", "239479:312-484396:25", "484396:25-597482:0"],
+     "N: 3, μ/σ: 194067/57877.4, med/mad: 224301/20521"),
+    ("240k", ["0:45846-263656:191", "263656:191-508565:287", "508565:287-597482:0"],
+     "N: 3, μ/σ: 194067/74433.1, med/mad: 244941/3497"),
+])
+def test_compute_splits_report(m, split_lines, stats, tmp_path):
+    from sbam import cli
+    out = tmp_path / "out.txt"
+    assert cli.main(["compute-splits", "-s", "-m", m, os.path.join(FIXTURES, "1.bam"), str(out)]) == 0
+    lines = out.read_text().split("\n")
+    assert re.fullmatch(r"Get spark-bam splits: \d+ms", lines[0])
+    assert lines[1:4] == ["", "Split-size distribution:", stats]
+    assert lines[6:] == ["", "3 splits:"] + ["\t" + s for s in split_lines] + ["", ""]
+
+
+@pytest.mark.gpu
+def test_count_reads_report(tmp_path):
+    # CountReadsTest.scala:10-20: 4917 reads in 1.bam at 240k
+    from sbam import cli
+    out = tmp_path / "out.txt"
+    assert cli.main(["count-reads", "-m", "240k", os.path.join(FIXTURES, "1.bam"), str(out)]) == 0
+    lines = out.read_text().split("\n")
+    assert re.fullmatch(r"spark-bam read-count time: \d+", lines[0])
+    assert lines[2] == "spark-bam found 4917 reads"
