@@ -1,6 +1,7 @@
 """spark-bam CLI drop-ins over the GPU path: `full-check`, `compute-splits -s`, `count-reads`.
 
     python -m sbam.cli full-check [-l LIMIT] [-m SPLIT] [-i RANGES] [-r READS] BAM [OUT]
+    python -m sbam.cli check-bam -s [-l LIMIT] [-m SPLIT] [-i RANGES] BAM [OUT]
     python -m sbam.cli compute-splits [-s] [-l LIMIT] [-m SPLIT] BAM [OUT]
     python -m sbam.cli count-reads [-m SPLIT] BAM [OUT]
 
@@ -9,6 +10,7 @@ verbatim (tests/test_cli.py):
   * full-check: FullCheck.scala:141-322, the CheckerApp summary (CheckerApp.scala:140-222) when a `.records`
     sidecar is present, PosMetadata / NextRecord (check/PosMetadata.scala, NextRecord.scala), Counts.lines
     (check/.../full/error/Counts.scala:59-127);
+  * check-bam -s: eager/CheckBam.scala + the CheckerApp comparison with the `.records` truth;
   * compute-splits: ComputeSplits.scala:56-68 (-s: spark-bam splits only; hadoop-bam comparison is out of scope);
   * count-reads: compare/CountReads.scala:80-100, spark-bam side only.
 Counting, checking and splitting all run through libsbam.so (sbam.BamFile); this module only formats."""
@@ -196,6 +198,58 @@ class FullCheckReport:
             a = b
         return None
 
+    def truth(self) -> set:
+        out = set()
+        for line in open(self.records_path):
+            if line.strip():
+                b, o = (int(v) for v in line.split(","))
+                out.add(self.f.offset_of(Pos(b, o)))
+        return out
+
+    def summary(self, calls_bits, n_positions):
+        """CheckerApp.scala:140-222: positions, compressed size, ratio, reads, then the comparison of the calls
+        with the `.records` truth (lines, false-positive offsets, false-negative offsets)."""
+        truth = self.truth()
+        tp, fps, fns = 0, [], []
+        for x0, bits in calls_bits:
+            called = set((x0 + np.nonzero(bits)[0]).tolist())
+            expected = {t for t in truth if x0 <= t < x0 + bits.size}
+            tp += len(called & expected)
+            fps += sorted(called - expected)
+            fns += sorted(expected - called)
+        ratio = n_positions / self.compressed if self.compressed else float("nan")
+        out = [f"{n_positions} uncompressed positions", f"{format_bytes(self.compressed)} compressed",
+               "Compression ratio: %.2f" % ratio, f"{tp + len(fns)} reads"]
+        if not fps and not fns:
+            out.append("All calls matched!")
+            return out, fps, fns
+        out += [f"{len(fps)} false positives, {len(fns)} false negatives", ""]
+        if fps:
+            words = {x: int(self.f.check_full_words(x, x + 1, self.R)[0]) for x in fps}
+            hist = {}
+            for x in fps:
+                F = words[x] & 0x7ffff
+                hist[F] = hist.get(F, 0) + 1
+            rows = sorted(hist.items(), key=lambda kv: -kv[1])
+            print_limited(out, [f"{n}:\t{show_flags(F)}" for F, n in rows], None,
+                          "False-positive-site flags histogram:", lambda _: "False-positive-site flags histogram:",
+                          self.limit)
+            out.append("")
+            items = [self.pos_metadata(x, words[x]) for x in fps[:self.limit]]
+            print_limited(out, items, len(fps), "False positives with succeeding read info:",
+                          lambda n: f"{n} of {len(fps)} false positives with succeeding read info::", self.limit)
+        if fns:
+            print_limited(out, [str(self.f.pos_of(x)) for x in fns[:self.limit]], len(fns),
+                          f"{len(fns)} false negatives:", lambda n: f"{n} of {len(fns)} false negatives:", self.limit)
+        return out, fps, fns
+
+    def check_bam_lines(self) -> List[str]:
+        """check-bam -s (eager/CheckBam.scala, vsIndexed): the eager checker at every position of the selected
+        blocks against the `.records` truth."""
+        calls_bits = [(x0, self.f.check_eager(x0, x1, self.R)) for x0, x1 in self.runs]
+        n_positions = sum(x1 - x0 for x0, x1 in self.runs)
+        return self.summary(calls_bits, n_positions)[0]
+
     def lines(self) -> List[str]:
         f, out = self.f, []
         counts = None
@@ -217,23 +271,10 @@ class FullCheckReport:
             n_success += c.n_success
             calls_bits.append((x0, bits))
         if self.records_path and os.path.exists(self.records_path):
-            truth = set()
-            for line in open(self.records_path):
-                if line.strip():
-                    b, o = (int(v) for v in line.split(","))
-                    truth.add(f.offset_of(Pos(b, o)))
-            tp = fp = fn = 0
-            for x0, bits in calls_bits:
-                called = set((x0 + np.nonzero(bits)[0]).tolist())
-                expected = {t for t in truth if x0 <= t < x0 + bits.size}
-                tp += len(called & expected)
-                fp += len(called - expected)
-                fn += len(expected - called)
-            if fp or fn:  # FullCheck.scala:108-114: a mismatch is an error
-                raise RuntimeError(f"{fp} false positives, {fn} false negatives against {self.records_path}")
-            ratio = n_positions / self.compressed if self.compressed else float("nan")
-            out += [f"{n_positions} uncompressed positions", f"{format_bytes(self.compressed)} compressed",
-                    "Compression ratio: %.2f" % ratio, f"{tp + fn} reads", "All calls matched!", ""]
+            head, fp, fn = self.summary(calls_bits, n_positions)
+            if fp or fn:  # FullCheck.scala:108-114: a full-check call disagreeing with the records is an error
+                raise RuntimeError(f"{len(fp)} false positives, {len(fn)} false negatives against {self.records_path}")
+            out += head + [""]
         field_names = FLAG_NAMES[:19]
 
         def pairs(vec):
@@ -347,16 +388,16 @@ def count_reads_lines(f: sbam.BamFile, split_size: int) -> List[str]:
 def main(argv: Optional[Sequence[str]] = None) -> int:
     ap = argparse.ArgumentParser(prog="sbam.cli")
     sub = ap.add_subparsers(dest="cmd", required=True)
-    for name in ("full-check", "compute-splits", "count-reads"):
+    for name in ("full-check", "check-bam", "compute-splits", "count-reads"):
         p = sub.add_parser(name)
         p.add_argument("-l", "--print-limit", type=int, default=10)
         p.add_argument("-m", "--max-split-size", type=parse_bytes, default=2 << 20)
         p.add_argument("bam")
         p.add_argument("out", nargs="?")
-        if name == "full-check":
+        if name in ("full-check", "check-bam"):
             p.add_argument("-i", "--intervals", type=parse_ranges, default=None)
             p.add_argument("-r", "--reads-to-check", type=int, default=10)
-        if name == "compute-splits":
+        if name in ("compute-splits", "check-bam"):
             p.add_argument("-s", "--spark-bam", action="store_true")
     a = ap.parse_args(argv)
     data = open(a.bam, "rb").read()
@@ -364,6 +405,11 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
         if a.cmd == "full-check":
             rep = FullCheckReport(f, data, a.bam + ".records", a.print_limit, a.intervals, a.reads_to_check)
             lines = rep.lines()
+        elif a.cmd == "check-bam":
+            rep = FullCheckReport(f, data, a.bam + ".records", a.print_limit, a.intervals, a.reads_to_check)
+            if not os.path.exists(rep.records_path):
+                raise SystemExit(f"check-bam -s needs the indexed records {rep.records_path} (index-records)")
+            lines = rep.check_bam_lines()
         elif a.cmd == "compute-splits":
             lines = compute_splits_lines(f, a.max_split_size, a.print_limit)
         else:

@@ -131,6 +131,30 @@ def test_compute_splits_report(m, split_lines, stats, tmp_path):
     assert lines[6:] == ["", "3 splits:"] + ["\t" + s for s in split_lines] + ["", ""]
 
 
+def test_check_bam_logic():
+    """check-bam -s summary on the oracle backend: CheckBamTest.scala "eager 1.bam" (no false calls)."""
+    from sbam import cli
+    data = open(os.path.join(FIXTURES, "1.bam"), "rb").read()
+    rep = cli.FullCheckReport(OracleBam(data), data, os.path.join(FIXTURES, "1.bam.records"), 10)
+    assert rep.check_bam_lines() == CHECK_BAM_EAGER_1
+
+
+CHECK_BAM_EAGER_1 = ["1608257 uncompressed positions", "583K compressed", "Compression ratio: 2.69", "4917 reads",
+                     "All calls matched!"]
+
+
+@pytest.mark.gpu
+def test_check_bam_report(tmp_path):
+    # CheckBamTest.scala:40-50 ("eager 1.bam", -m 200k)
+    from sbam import cli
+    path = tmp_path / "1.bam"
+    shutil.copy(os.path.join(FIXTURES, "1.bam"), path)
+    shutil.copy(os.path.join(FIXTURES, "1.bam.records"), str(path) + ".records")
+    out = tmp_path / "out.txt"
+    assert cli.main(["check-bam", "-s", "-m", "200k", str(path), str(out)]) == 0
+    assert out.read_text() == "\n".join(CHECK_BAM_EAGER_1) + "\n"
+
+
 @pytest.mark.gpu
 def test_count_reads_report(tmp_path):
     # CountReadsTest.scala:10-20: 4917 reads in 1.bam at 240k
