@@ -99,20 +99,26 @@ def main():
                     help="sequential byte-range windows per GPU: streams a shard larger than HBM through one "
                          "device (each window: its own load + halo; PCIe copy inside the timed step)")
     ap.add_argument("--read-len", type=int, default=150, help="0 = long-read config (configs[4])")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (RCCL, the product path); gloo only to rehearse N ranks on one GPU (--device)")
+    ap.add_argument("--device", type=int, default=None, help="GPU index (default LOCAL_RANK)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    local = int(os.environ.get("LOCAL_RANK", 0)) if args.device is None else args.device
     import torch
+    torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
     else:
         dist = None
-        torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    cdev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # collective tensors
 
     import sbam
     import synth
@@ -169,7 +175,7 @@ def main():
                                     *(np.concatenate([getattr(r, a) for r in parts]) for a in
                                       ("first_block_pos", "first_offset", "nonempty", "n_records")))
         if world > 1 and args.workload == "full-check":
-            sdist.gather_results(res, plans, device=dev)
+            sdist.gather_results(res, plans, device=cdev)
         return res, ms
 
     def sync():
@@ -192,7 +198,7 @@ def main():
     sync()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
@@ -203,7 +209,7 @@ def main():
         counts["n_success"] = n_rec
     ok_local = counts["n_success"] == int(res.n_records.sum()) if world == 1 else True
     if world > 1:
-        v = torch.tensor([counts["n_success"], n_rec], dtype=torch.int64, device=dev)
+        v = torch.tensor([counts["n_success"], n_rec], dtype=torch.int64, device=cdev)
         dist.all_reduce(v)
         tot_succ, tot_rec = (int(x) for x in v.tolist())
     else:
