@@ -1,7 +1,11 @@
-"""spark-bam CLI drop-ins over the GPU path: `full-check`, `compute-splits -s`, `count-reads`.
+"""spark-bam CLI drop-ins over the GPU path: `full-check`, `check-bam -s`, `check-blocks -s`, `compute-splits -s`,
+`count-reads`, `index-blocks`, `index-records`.
 
     python -m sbam.cli full-check [-l LIMIT] [-m SPLIT] [-i RANGES] [-r READS] BAM [OUT]
     python -m sbam.cli check-bam -s [-l LIMIT] [-m SPLIT] [-i RANGES] BAM [OUT]
+    python -m sbam.cli check-blocks -s [-l LIMIT] BAM [OUT]
+    python -m sbam.cli index-blocks BAM [OUT]
+    python -m sbam.cli index-records BAM [OUT]
     python -m sbam.cli compute-splits [-s] [-l LIMIT] [-m SPLIT] BAM [OUT]
     python -m sbam.cli count-reads [-m SPLIT] BAM [OUT]
 
@@ -11,6 +15,9 @@ verbatim (tests/test_cli.py):
     sidecar is present, PosMetadata / NextRecord (check/PosMetadata.scala, NextRecord.scala), Counts.lines
     (check/.../full/error/Counts.scala:59-127);
   * check-bam -s: eager/CheckBam.scala + the CheckerApp comparison with the `.records` truth;
+  * check-blocks -s: blocks/CheckBlocks.scala (eager vs indexed first read per block);
+  * index-blocks / index-records: bgzf/.../index/IndexBlocks.scala, check/.../bam/index/IndexRecords.scala (the
+    `.blocks` / `.records` sidecars);
   * compute-splits: ComputeSplits.scala:56-68 (-s: spark-bam splits only; hadoop-bam comparison is out of scope);
   * count-reads: compare/CountReads.scala:80-100, spark-bam side only.
 Counting, checking and splitting all run through libsbam.so (sbam.BamFile); this module only formats."""
@@ -385,10 +392,128 @@ def count_reads_lines(f: sbam.BamFile, split_size: int) -> List[str]:
     return [f"spark-bam read-count time: {ms}", "", f"spark-bam found {n} reads", ""]
 
 
+# ---- check-blocks -s / index-blocks / index-records ------------------------------------------------------------
+def _jround(v: float) -> int:
+    """java.lang.Math.round: floor(x + 0.5)."""
+    return int(math.floor(v + 0.5))
+
+
+def hist_stats_lines(hist: Sequence[Tuple[int, int]]) -> List[str]:
+    """hammerlab Stats.fromHist with Show[Double] = math.round (CheckBlocks.scala:135-150): N, mean/population σ,
+    median/MAD; the (value, count) entries in value order (`v×c` for repeats, first 10 … last 10 past 20
+    entries); percentiles by linear interpolation at rank p(N+1)/100, printed for the p whose rank lies in
+    [1, N].  Pinned by the CheckBlocksTest goldens (N = 25); other sizes are parity unpinned."""
+    hist = sorted((int(v), int(c)) for v, c in hist if c > 0)
+    vals = np.repeat(np.array([v for v, _ in hist], np.float64), [c for _, c in hist])
+    n = vals.size
+    if n == 0:
+        return ["N: 0"]
+    mean = vals.mean()
+    sd = math.sqrt(((vals - mean) ** 2).mean())
+    med = float(np.median(vals))
+    mad = float(np.median(np.abs(vals - med)))
+    out = [f"N: {n}, μ/σ: {_jround(mean)}/{_jround(sd)}, med/mad: {_jround(med)}/{_jround(mad)}"]
+    ent = [str(v) if c == 1 else f"{v}×{c}" for v, c in hist]
+    if len(ent) > 20:
+        ent = ent[:10] + ["…"] + ent[-10:]
+    out.append(" elems: " + " ".join(ent))
+    for p in (1, 5, 10, 25, 50, 75, 90, 95, 99):
+        r = p * (n + 1) / 100.0
+        if r < 1 or r > n:
+            continue
+        i = int(math.floor(r)) - 1
+        v = vals[i] + (r - 1 - i) * (vals[min(i + 1, n - 1)] - vals[i])
+        out.append(f"{p:>4}:\t{_jround(v)}")
+    return out
+
+
+def _next_start(sorted_offs: np.ndarray, x: int) -> Optional[int]:
+    i = int(np.searchsorted(sorted_offs, x))
+    return int(sorted_offs[i]) if i < sorted_offs.size else None
+
+
+def check_blocks_lines(f: sbam.BamFile, truth_offsets: np.ndarray, limit: int,
+                       reads_to_check: int = sbam.READS_TO_CHECK) -> List[str]:
+    """check-blocks -s (cli/.../check/blocks/CheckBlocks.scala:37-190): per BGZF block, the eager checker's
+    nextReadStart(Pos(start, 0)) (GPU bitmap) against the indexed checker's (the `.records` truth,
+    check/.../indexed/Checker.scala:12-27); blocks whose answers differ, weighted by the previous block's
+    compressed size, and the histogram of the blocks' first-read offsets."""
+    st, cs, us, uo = f.blocks()
+    L = f.uncompressed_size
+    eager = np.flatnonzero(f.check_eager(0, L, reads_to_check)).astype(np.int64)
+    truth = np.sort(np.asarray(truth_offsets, np.int64))
+
+    def pos(x):
+        return None if x is None else f.pos_of(x)
+
+    bad, offs = [], {}
+    for b in range(st.size):
+        p1, p2 = pos(_next_start(eager, int(uo[b]))), pos(_next_start(truth, int(uo[b])))
+        off = p1.offset if p1 is not None and p1.block_pos == int(st[b]) else None
+        offs[off] = offs.get(off, 0) + 1
+        if (str(p1) if p1 else None) != (str(p2) if p2 else None):
+            bad.append((int(st[b]), p1, p2, int(cs[b - 1]) if b > 0 else 1))
+    size = f.file_size
+    n_blocks = int(st.size)
+    out: List[str] = []
+
+    def offsets_info():
+        keys = set(offs)
+        if keys == {None, 0}:
+            out.extend(["", f"{offs[0]} blocks start with a read, {offs[None]} blocks didn't contain a read"])
+        elif keys == {0}:
+            out.extend(["", "All blocks start with reads"])
+        else:
+            out.extend(["", f"Offsets of blocks' first reads ({offs.get(None, 0)} blocks didn't contain a read "
+                            "start):"])
+            out.extend(hist_stats_lines([(k, v) for k, v in offs.items() if k is not None]))
+
+    if not bad:
+        out.append(f"First read-position matched in {n_blocks} BGZF blocks totaling {format_bytes(size)}B "
+                   "(compressed)")
+        offsets_info()
+    else:
+        wc = sum(w for *_, w in bad)
+        out += [f"First read-position mismatched in {len(bad)} of {n_blocks} BGZF blocks", "",
+                f"{wc} of {size} ({repr(wc / size)}) compressed positions would lead to bad splits"]
+        offsets_info()
+        out.append("")
+        items = [f"{s} (prev block size: {w}):\t{p1 if p1 else '-'}\t{p2 if p2 else '-'}" for s, p1, p2, w in bad]
+        print_limited(out, items, None, f"{len(bad)} mismatched blocks:",
+                      lambda n: f"{n} of {len(bad)} mismatched blocks:", limit)
+    return out
+
+
+def index_blocks_lines(f: sbam.BamFile) -> List[str]:
+    """IndexBlocks (bgzf/.../index/IndexBlocks.scala:24-45): `start,compressedSize,uncompressedSize` per block of
+    the MetadataStream (which stops at the first empty block), from the GPU header scan."""
+    st, cs, us, _ = f.blocks()
+    return [f"{a},{b},{c}" for a, b, c in zip(st.tolist(), cs.tolist(), us.tolist())]
+
+
+def index_records_lines(f: sbam.BamFile) -> List[str]:
+    """IndexRecords (check/.../bam/index/IndexRecords.scala:36-90, PosStream): `blockPos,offset` of every record
+    start from the end of the BAM header, chained by block_size (PosStream.scala:14-22).  PosStream emits a
+    record's Pos once its 4-byte block_size is read and drops the rest lazily, so a truncated last record is
+    still listed and ends the stream.  (A negative block_size, which PosStream would step over by 4 bytes, ends
+    the listing here: parity unpinned, no fixture has one.)"""
+    f.header()
+    L = f.uncompressed_size
+    x0 = f.offset_of(f.header_end)
+    offs = [int(x) for x in f.record_offsets(x0, L)]
+    x = x0
+    if offs:
+        x = offs[-1] + 4 + int.from_bytes(f.read_uncompressed(offs[-1], 4), "little", signed=True)
+    if x + 4 <= L and int.from_bytes(f.read_uncompressed(x, 4), "little", signed=True) >= 0:
+        offs.append(x)  # truncated last record
+    return [str(f.pos_of(x)).replace(":", ",") for x in offs]
+
+
 def main(argv: Optional[Sequence[str]] = None) -> int:
     ap = argparse.ArgumentParser(prog="sbam.cli")
     sub = ap.add_subparsers(dest="cmd", required=True)
-    for name in ("full-check", "check-bam", "compute-splits", "count-reads"):
+    for name in ("full-check", "check-bam", "check-blocks", "compute-splits", "count-reads", "index-blocks",
+                 "index-records"):
         p = sub.add_parser(name)
         p.add_argument("-l", "--print-limit", type=int, default=10)
         p.add_argument("-m", "--max-split-size", type=parse_bytes, default=2 << 20)
@@ -397,7 +522,7 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
         if name in ("full-check", "check-bam"):
             p.add_argument("-i", "--intervals", type=parse_ranges, default=None)
             p.add_argument("-r", "--reads-to-check", type=int, default=10)
-        if name in ("compute-splits", "check-bam"):
+        if name in ("compute-splits", "check-bam", "check-blocks"):
             p.add_argument("-s", "--spark-bam", action="store_true")
     a = ap.parse_args(argv)
     data = open(a.bam, "rb").read()
@@ -410,6 +535,17 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
             if not os.path.exists(rep.records_path):
                 raise SystemExit(f"check-bam -s needs the indexed records {rep.records_path} (index-records)")
             lines = rep.check_bam_lines()
+        elif a.cmd == "check-blocks":
+            rp = a.bam + ".records"
+            if not a.spark_bam or not os.path.exists(rp):
+                raise SystemExit("check-blocks runs as -s (spark-bam eager checker vs the indexed records "
+                                 f"{rp}); the hadoop-bam comparison is out of scope")
+            truth = [f.offset_of(Pos(*(int(v) for v in ln.split(",")))) for ln in open(rp) if ln.strip()]
+            lines = check_blocks_lines(f, np.asarray(truth, np.int64), a.print_limit)
+        elif a.cmd == "index-blocks":
+            lines = index_blocks_lines(f)
+        elif a.cmd == "index-records":
+            lines = index_records_lines(f)
         elif a.cmd == "compute-splits":
             lines = compute_splits_lines(f, a.max_split_size, a.print_limit)
         else:
