@@ -176,6 +176,11 @@ int sbam_compute_splits(sbam_ctx *ctx, const sbam_split_args *args, sbam_split *
  * (cap entries) and *n_out records; record bytes are stream[off, off+4+block_size). */
 int sbam_record_offsets(sbam_ctx *ctx, int64_t x0, int64_t x_end, int64_t *offsets, int64_t cap, int64_t *n_out);
 
+/* Reference spans of the records at the n stream offsets (loadBamIntervals' region filter, CanLoadBam.scala:
+ * 107-135, 423-431): ref_id, start = POS (0-based) and end = POS + the CIGAR's reference length (M/D/N/=/X),
+ * i.e. [getStart - 1, getEnd); unmapped records (flag 4) get end = 0, htsjdk's getAlignmentEnd. */
+int sbam_record_spans(sbam_ctx *ctx, const int64_t *offsets, int64_t n, int32_t *ref_id, int32_t *start, int32_t *end);
+
 /* ---- record decode: loadReads / loadReadsAndPositions (CanLoadBam.scala:221-241, 281-334) ------------- */
 
 /* Per-record columns: the record's flat stream offset, its Pos, and the BAM fixed fields (SAM spec §4.2, the

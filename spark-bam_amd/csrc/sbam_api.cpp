@@ -942,6 +942,27 @@ int sbam_record_offsets(sbam_ctx *c, int64_t x0, int64_t x_end, int64_t *offsets
   return SBAM_OK;
 }
 
+int sbam_record_spans(sbam_ctx *c, const int64_t *offsets, int64_t n, int32_t *ref_id, int32_t *start, int32_t *end) {
+  if (!c || n < 0 || (n && (!offsets || !ref_id || !start || !end))) return SBAM_ERR_ARG;
+  if (n == 0) return SBAM_OK;
+  int rc = ensure_stream(c);
+  if (rc) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  int64_t *d_o = nullptr;
+  int32_t *d_r = nullptr;
+  HIPCHK(c, dalloc(&d_o, n));
+  HIPCHK(c, dalloc(&d_r, 3 * n));
+  HIPCHK(c, hipMemcpyAsync(d_o, offsets, n * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, launch_record_spans(c->d_u, c->L, d_o, n, d_r, d_r + n, d_r + 2 * n, c->stream));
+  HIPCHK(c, hipMemcpyAsync(ref_id, d_r, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(start, d_r + n, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(end, d_r + 2 * n, n * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  dfree(d_o);
+  dfree(d_r);
+  return SBAM_OK;
+}
+
 // ---- record decode ---------------------------------------------------------------------------------------
 int sbam_load_records(sbam_ctx *c, const sbam_split_args *a, int64_t first, int64_t count, int64_t *split_counts_out,
                       int64_t *n_records) {

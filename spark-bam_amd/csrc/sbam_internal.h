@@ -110,6 +110,8 @@ hipError_t launch_split_offsets(const unsigned long long *bm, int64_t xa, const 
                                 const int64_t *base, int64_t n, int64_t *out, hipStream_t s);
 hipError_t launch_record_walk(const uint8_t *u, int64_t L, const int64_t *xs, const int64_t *xe, const int64_t *base,
                               int64_t n, int64_t *out, hipStream_t s);
+hipError_t launch_record_spans(const uint8_t *u, int64_t L, const int64_t *offs, int64_t n, int32_t *ref_id,
+                               int32_t *start, int32_t *end, hipStream_t s);
 hipError_t launch_record_columns(const uint8_t *u, const int64_t *offs, int64_t n, const int64_t *bstart,
                                  const int64_t *buoff, const int32_t *busize, int64_t nblocks, int64_t file_base,
                                  RecordColumnsDev cols, hipStream_t s);

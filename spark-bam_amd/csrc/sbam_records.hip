@@ -207,6 +207,44 @@ __global__ void k_record_columns(const uint8_t *__restrict__ u, const int64_t *_
   cols.tlen[i] = (int32_t)f[8];
 }
 
+// Reference span of the record at offs[i], as CanLoadBam.region reads it from htsjdk (CanLoadBam.scala:423-431):
+// refID, start = pos (= getStart - 1) and the exclusive end getEnd = pos + the CIGAR's reference length (ops M, D,
+// N, =, X: SAM spec §1.4.6).  An unmapped record (flag 4) has getAlignmentEnd = 0, so end = 0.  Ops past the
+// stream end are not read.
+__global__ void k_record_spans(const uint8_t *__restrict__ u, int64_t L, const int64_t *__restrict__ offs, int64_t n,
+                               int32_t *__restrict__ ref_id, int32_t *__restrict__ start, int32_t *__restrict__ end) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t x = offs[i];
+  if (x < 0 || x + 36 > L) {
+    ref_id[i] = -1;
+    start[i] = -1;
+    end[i] = 0;
+    return;
+  }
+  const int32_t ri = rd_i32(u, x + 4), pos = rd_i32(u, x + 8);
+  const uint32_t bmn = (uint32_t)rd_i32(u, x + 12), fnc = (uint32_t)rd_i32(u, x + 16);
+  const uint32_t nc = fnc & 0xffffu, flag = fnc >> 16;
+  int64_t c = x + 36 + (bmn & 0xffu);
+  int64_t rlen = 0;
+  for (uint32_t k = 0; k < nc && c + 4 <= L; k++, c += 4) {
+    const uint32_t op = (uint32_t)rd_i32(u, c);
+    const uint32_t t = op & 0xfu;
+    if (t == 0 || t == 2 || t == 3 || t == 7 || t == 8) rlen += op >> 4;
+  }
+  ref_id[i] = ri;
+  start[i] = pos;
+  end[i] = (flag & 4u) ? 0 : (int32_t)(pos + rlen);
+}
+
+hipError_t launch_record_spans(const uint8_t *u, int64_t L, const int64_t *offs, int64_t n, int32_t *ref_id,
+                               int32_t *start, int32_t *end, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_record_spans, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, u, L, offs, n, ref_id, start,
+                     end);
+  return hipGetLastError();
+}
+
 hipError_t launch_chain_proof(const uint8_t *u, int64_t L, const unsigned long long *bm, int64_t xa, int64_t X0,
                               int64_t X1, int32_t *fail, hipStream_t s) {
   if (X1 <= X0) return hipSuccess;

@@ -114,7 +114,7 @@ EXPORTS = [  # every symbol include/sbam.h declares
     "sbam_get_blocks", "sbam_inflate", "sbam_read_uncompressed", "sbam_pos_to_offset", "sbam_offset_to_pos",
     "sbam_header", "sbam_set_contig_lengths", "sbam_check_eager", "sbam_check_full_words", "sbam_check_full_counts",
     "sbam_find_record_start", "sbam_file_splits", "sbam_split_records", "sbam_compute_splits",
-    "sbam_record_offsets", "sbam_load_records", "sbam_get_record_columns", "sbam_record_columns_device",
+    "sbam_record_offsets", "sbam_record_spans", "sbam_load_records", "sbam_get_record_columns", "sbam_record_columns_device",
     "sbam_last_kernel_ms",
 ]
 
@@ -153,6 +153,7 @@ def load_library(path: str = LIB_PATH):
         "sbam_split_records": (ctypes.c_int, [vp, P(_SplitArgs), i64, i64, vp, vp, vp]),
         "sbam_compute_splits": (ctypes.c_int, [vp, P(_SplitArgs), vp, i64, P(i64)]),
         "sbam_record_offsets": (ctypes.c_int, [vp, i64, i64, vp, i64, P(i64)]),
+        "sbam_record_spans": (ctypes.c_int, [vp, vp, i64, vp, vp, vp]),
         "sbam_load_records": (ctypes.c_int, [vp, P(_SplitArgs), i64, i64, vp, P(i64)]),
         "sbam_get_record_columns": (ctypes.c_int, [vp, i64, i64, P(_RecordColumns)]),
         "sbam_record_columns_device": (ctypes.c_int, [vp, P(_RecordColumns), P(i64)]),
@@ -500,6 +501,61 @@ class BamFile:
         rc = _RecordColumns(**{k: v.ctypes.data for k, v in cols.items()})
         self._check(self.L.sbam_get_record_columns(self.ctx, 0, n.value, ctypes.byref(rc)))
         return sizes, cols
+
+    def record_spans(self, offsets: np.ndarray):
+        """(ref_id, start, end) of the records at `offsets`: [getStart - 1, getEnd) as CanLoadBam.region uses it
+        (unmapped: end 0)."""
+        offs = np.ascontiguousarray(offsets, np.int64)
+        n = offs.size
+        r, a, b = (np.zeros(n, np.int32) for _ in range(3))
+        self._check(self.L.sbam_record_spans(self.ctx, _ptr(offs), n, _ptr(r), _ptr(a), _ptr(b)))
+        return r, a, b
+
+    def _vpos_offset(self, v: int) -> int:
+        """Stream offset of an htsjdk virtual offset (block << 16 | offset); a block at or past the end of the
+        stream (the EOF marker) maps to the stream end."""
+        st, _, us, uo = self.blocks()
+        b, o = v >> 16, v & 0xffff
+        i = int(np.searchsorted(st, b))
+        if i < st.size and int(st[i]) == b:
+            return int(uo[i]) + min(o, int(us[i]))
+        if i >= st.size:
+            return self.uncompressed_size
+        raise SbamError(f"no BGZF block at {b}")
+
+    def load_bam_intervals(self, bai: bytes, loci: str, split_size: int = 32 << 20, ratio: float = 3.0):
+        """sc.loadBamIntervals (CanLoadBam.scala:59-138): the BAI chunks overlapping `loci` (htsjdk getFileSpan,
+        sbam.bai), grouped into partitions by estimated size (cappedCostGroups), and per chunk the records from
+        chunk.start while Pos < chunk.end whose [getStart - 1, getEnd) intersects the loci.  Record chains and
+        reference spans run on the GPU (sbam_record_offsets, sbam_record_spans).  Returns (chunks, partitions):
+        partitions = per partition, the record stream offsets kept, in file order.  (The MaxSplitSize default of
+        32 MiB is hammerlab's, outside the reference tree: parity unpinned.)"""
+        from sbam import bai as B
+        from sbam.cli import header_names
+        refs = B.parse_bai(bai)
+        names = header_names(self)
+        q = []
+        for contig, a, e in B.parse_loci(loci):
+            ri = names.index(contig) if contig in names else -1
+            q.append((ri, a + 1, e if e is not None else 0))  # toHtsJDKIntervals: 1-based closed
+        chunks = B.file_span(refs, q)
+        groups = B.capped_cost_groups([c.size(ratio) for c in chunks], float(split_size))
+        want = [(names.index(c) if c in names else -2, a, e) for c, a, e in B.parse_loci(loci)]
+        parts = []
+        for g in groups:
+            kept = []
+            for ci in g:
+                c = chunks[ci]
+                offs = self.record_offsets(self._vpos_offset(c.start), self._vpos_offset(c.end))
+                if offs.size == 0:
+                    continue
+                ri, st, en = self.record_spans(offs)
+                m = np.zeros(offs.size, bool)
+                for r, a, e in want:
+                    m |= (ri == r) & (st < (e if e is not None else 1 << 31)) & (en > a)
+                kept.append(offs[m])
+            parts.append(np.concatenate(kept) if kept else np.zeros(0, np.int64))
+        return chunks, parts
 
     def load_reads_and_positions(self, split_size: int, **kw):
         """loadReadsAndPositions: per partition, list of (Pos, record bytes) (CanLoadBam.scala:281-334).  Record
