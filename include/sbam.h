@@ -88,6 +88,12 @@ typedef struct {
 int sbam_open(int device, const uint8_t *data, int64_t len, int64_t base_offset, int64_t file_size,
               sbam_ctx **out);
 void sbam_close(sbam_ctx *ctx);
+/* Replace the resident compressed bytes of an open context with another byte range (of the same or another
+ * file) and drop every derived stage, keeping the device allocations: the streaming form of sbam_open for
+ * inputs larger than HBM, one byte-range window after another (a Spark task re-opening its channel at the
+ * next split range).  `data` may be pinned host memory; the copy is on the context's stream, so a second
+ * context can load the next window while this one computes. */
+int sbam_load(sbam_ctx *ctx, const uint8_t *data, int64_t len, int64_t base_offset, int64_t file_size);
 const sbam_error *sbam_last_error(const sbam_ctx *ctx);
 /* Drop every derived stage (block table, stream, bitmap) but keep the compressed bytes and the device
  * allocations, so the pipeline can be re-run from the resident input without allocating (bench). */

@@ -23,6 +23,7 @@ struct sbam_ctx {
   hipStream_t stream = nullptr;
   int64_t D = 0, base = 0, file_size = 0;
   uint8_t *d_comp = nullptr;
+  size_t comp_cap = 0;
   // candidates from the header scan
   Candidate *d_cand = nullptr;
   int64_t ncand = -1;
@@ -219,7 +220,7 @@ int sbam_open(int device, const uint8_t *data, int64_t len, int64_t base_offset,
   c->file_size = file_size;
   HIPCHK(c, hipSetDevice(device));
   HIPCHK(c, hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HIPCHK(c, dalloc(&c->d_comp, (size_t)len + kCompPad));
+  HIPCHK(c, ensure(&c->d_comp, &c->comp_cap, (size_t)len + kCompPad));
   HIPCHK(c, hipMemsetAsync(c->d_comp + len, 0, kCompPad, c->stream));
   if (len) HIPCHK(c, hipMemcpyAsync(c->d_comp, data, (size_t)len, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, dalloc(&c->d_small, 64));
@@ -267,6 +268,20 @@ void sbam_close(sbam_ctx *c) {
 }
 
 const sbam_error *sbam_last_error(const sbam_ctx *c) { return c ? &c->err : nullptr; }
+
+int sbam_load(sbam_ctx *c, const uint8_t *data, int64_t len, int64_t base_offset, int64_t file_size) {
+  if (!c || (!data && len > 0) || len < 0 || base_offset < 0 || file_size < base_offset + len) return SBAM_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // the previous window's work is done with d_comp
+  HIPCHK(c, ensure(&c->d_comp, &c->comp_cap, (size_t)len + kCompPad));
+  HIPCHK(c, hipMemsetAsync(c->d_comp + len, 0, kCompPad, c->stream));
+  if (len) HIPCHK(c, hipMemcpyAsync(c->d_comp, data, (size_t)len, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->D = len;
+  c->base = base_offset;
+  c->file_size = file_size;
+  return sbam_reset(c);
+}
 
 int sbam_reset(sbam_ctx *c) {
   if (!c) return SBAM_ERR_ARG;

@@ -110,7 +110,7 @@ RECORD_COLUMNS = {"offset": np.int64, "block_pos": np.int64, "block_off": np.int
 
 
 EXPORTS = [  # every symbol include/sbam.h declares
-    "sbam_open", "sbam_close", "sbam_last_error", "sbam_reset", "sbam_version", "sbam_find_block_starts", "sbam_scan_blocks",
+    "sbam_open", "sbam_close", "sbam_load", "sbam_last_error", "sbam_reset", "sbam_version", "sbam_find_block_starts", "sbam_scan_blocks",
     "sbam_get_blocks", "sbam_inflate", "sbam_read_uncompressed", "sbam_pos_to_offset", "sbam_offset_to_pos",
     "sbam_header", "sbam_set_contig_lengths", "sbam_check_eager", "sbam_check_full_words", "sbam_check_full_counts",
     "sbam_find_record_start", "sbam_file_splits", "sbam_split_records", "sbam_compute_splits",
@@ -153,6 +153,7 @@ def load_library(path: str = LIB_PATH):
         "sbam_split_records": (ctypes.c_int, [vp, P(_SplitArgs), i64, i64, vp, vp, vp]),
         "sbam_compute_splits": (ctypes.c_int, [vp, P(_SplitArgs), vp, i64, P(i64)]),
         "sbam_record_offsets": (ctypes.c_int, [vp, i64, i64, vp, i64, P(i64)]),
+        "sbam_load": (ctypes.c_int, [vp, vp, i64, i64, i64]),
         "sbam_record_spans": (ctypes.c_int, [vp, vp, i64, vp, vp, vp]),
         "sbam_load_records": (ctypes.c_int, [vp, P(_SplitArgs), i64, i64, vp, P(i64)]),
         "sbam_get_record_columns": (ctypes.c_int, [vp, i64, i64, P(_RecordColumns)]),
@@ -289,6 +290,17 @@ class BamFile:
             self.close()
         except Exception:
             pass
+
+    def load(self, data, base_offset: int = 0, file_size: Optional[int] = None):
+        """sbam_load: make another byte range resident in this context (allocations kept, stages dropped).
+        `data` (numpy uint8, possibly a view of pinned host memory) must stay alive while loading."""
+        buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        self._buf = np.ascontiguousarray(buf)
+        self.base_offset = base_offset
+        self.file_size = int(file_size if file_size is not None else base_offset + self._buf.size)
+        self._check(self.L.sbam_load(self.ctx, _ptr(self._buf), self._buf.size, base_offset, self.file_size))
+        self.n_blocks = None
+        self.uncompressed_size = None
 
     def reset(self):
         """Drop derived stages (keeps the resident compressed bytes and allocations)."""

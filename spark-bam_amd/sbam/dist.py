@@ -138,6 +138,13 @@ class GpuShard:
         self.f = self.sbam.BamFile(self.source(lo, hi), device=self.device, base_offset=lo,
                                    file_size=self.plan.file_size, inflate=False)
 
+    def reload(self, plan: ShardPlan, data: np.ndarray):
+        """Stream the next byte-range window through this shard's context (sbam_load: device allocations are
+        kept): `data` = the bytes of plan.load_range(self.halo)."""
+        self.plan = plan
+        lo, _ = plan.load_range(self.halo)
+        self.f.load(data, base_offset=lo, file_size=plan.file_size)
+
     def _once(self) -> ShardResult:
         self.f.reset()
         self.f.run(contig_lengths=self.contig_lengths)

@@ -47,3 +47,34 @@ def test_library_is_gfx950_code_object():
     so = os.path.join(ROOT, "spark-bam_amd", "build", "libsbam.so")
     data = open(so, "rb").read()
     assert b"gfx950" in data
+
+
+def test_load_replaces_window_on_gpu_marker():
+    """(CPU) sbam_load is declared and bound like sbam_open (GPU behaviour: test_load_window_gpu)."""
+    import sbam
+    assert "sbam_load" in sbam.EXPORTS
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_load_window_gpu():
+    """sbam_load: a context re-filled with another file (and back) gives the same blocks, stream and checker
+    calls as a fresh sbam_open of that file, with its allocations reused."""
+    import numpy as np
+    import sbam
+    from conftest import fixture_bytes
+    a, b = fixture_bytes("1.bam"), fixture_bytes("2.bam")
+    with sbam.BamFile(b) as fresh:
+        want_blocks = [x.copy() for x in fresh.blocks()]
+        want_calls = fresh.check_eager(0, fresh.uncompressed_size)
+    with sbam.BamFile(a) as f:
+        for _ in range(2):
+            f.load(b)
+            f.run()
+            assert all(np.array_equal(x, y) for x, y in zip(f.blocks(), want_blocks))
+            assert np.array_equal(f.check_eager(0, f.uncompressed_size), want_calls)
+            f.load(a)
+            f.run()
+            assert f.blocks()[0].size == 25 and int(f.check_eager(0, f.uncompressed_size).sum()) == 4917
