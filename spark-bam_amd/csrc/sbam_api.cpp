@@ -24,6 +24,12 @@ struct sbam_ctx {
   int64_t D = 0, base = 0, file_size = 0;
   uint8_t *d_comp = nullptr;
   size_t comp_cap = 0;
+  // list-form chain pass scratch (launch_chain_list_*)
+  int32_t *d_ccnt = nullptr;
+  int64_t *d_coff2 = nullptr, *d_plist = nullptr, *d_pfb = nullptr;
+  uint8_t *d_pok = nullptr;
+  unsigned long long *d_nfb = nullptr;
+  size_t ccnt_cap = 0, coff2_cap = 0, plist_cap = 0, pfb_cap = 0, pok_cap = 0, nfb_cap = 0;
   // candidates from the header scan
   Candidate *d_cand = nullptr;
   int64_t ncand = -1;
@@ -234,6 +240,12 @@ void sbam_close(sbam_ctx *c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   dfree(c->d_comp);
+  dfree(c->d_ccnt);
+  dfree(c->d_coff2);
+  dfree(c->d_plist);
+  dfree(c->d_pfb);
+  dfree(c->d_pok);
+  dfree(c->d_nfb);
   dfree(c->d_cand);
   dfree(c->d_cc);
   dfree(c->d_coff);
@@ -500,8 +512,10 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
     if (c->pool_cap > want) want = c->pool_cap;
     HIPCHK(c, ensure(&c->d_blkpage, &c->blkpage_cap, nb));
     if (!c->d_icnt) HIPCHK(c, dalloc(&c->d_icnt, 4));
-    const int dec_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256 * 2);
-    const int res_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256 * 4);
+    int dec_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256 * 2);
+    int res_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256 * 4);
+    if (const char *e = getenv("SBAM_DEC_WGS")) dec_wgs = std::max(1, atoi(e));  // A/B sweeps only
+    if (const char *e = getenv("SBAM_RES_WGS")) res_wgs = std::max(1, atoi(e));
     for (;;) {
       if (c->pool_cap < want) {
         dfree(c->d_pool);
@@ -696,6 +710,32 @@ int sbam_check_full_words(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, uint32
   return SBAM_OK;
 }
 
+// Chain pass after a record-0 pass: the list form (launch_chain_list_*) when the PASS0 positions fit its
+// scratch (a position list of up to 1/32 of the range), else the per-chunk k_chains walk.
+static hipError_t run_chains(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd) {
+  const int64_t nch = chain_list_chunks(x0, x1);
+  const int64_t cap = (x1 - x0) / 32 + 4096;
+  hipError_t e;
+  if ((e = ensure(&c->d_ccnt, &c->ccnt_cap, (size_t)std::max<int64_t>(nch, 1))) != hipSuccess) return e;
+  if ((e = ensure(&c->d_coff2, &c->coff2_cap, (size_t)nch + 1)) != hipSuccess) return e;
+  ChainScratch cs{c->d_ccnt, c->d_coff2, nullptr, nullptr, nullptr, nullptr};
+  if ((e = launch_chain_list_build(x0, x1, c->d_bitmap, cs, c->stream)) != hipSuccess) return e;
+  int64_t total = 0;
+  if ((e = hipMemcpyAsync(&total, c->d_coff2 + nch, 8, hipMemcpyDeviceToHost, c->stream)) != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return e;
+  if (total > cap) return launch_check_full_chains(view(c), x0, x1, R, by_key, cd, c->d_bitmap, c->stream);
+  const size_t n = (size_t)std::max<int64_t>(total, 1);
+  if ((e = ensure(&c->d_plist, &c->plist_cap, n)) != hipSuccess) return e;
+  if ((e = ensure(&c->d_pfb, &c->pfb_cap, n)) != hipSuccess) return e;
+  if ((e = ensure(&c->d_pok, &c->pok_cap, n)) != hipSuccess) return e;
+  if ((e = ensure(&c->d_nfb, &c->nfb_cap, 1)) != hipSuccess) return e;
+  cs.list = c->d_plist;
+  cs.ok = c->d_pok;
+  cs.fb = c->d_pfb;
+  cs.n_fb = c->d_nfb;
+  return launch_chain_list_run(view(c), x0, x1, R, by_key, cd, c->d_bitmap, cs, c->stream);
+}
+
 int sbam_check_full_counts(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, int32_t by_key, sbam_counts *out,
                            uint64_t *bitmap) {
   if (!c || !out) return SBAM_ERR_ARG;
@@ -719,7 +759,7 @@ int sbam_check_full_counts(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, int32
       HIPCHK(c, launch_check_full_counts(view(c), x0, x1, R, by_key, cd, c->d_bitmap, c->stream));
     }
     Timer t1(c, "check_chains");
-    HIPCHK(c, launch_check_full_chains(view(c), x0, x1, R, by_key, cd, c->d_bitmap, c->stream));
+    HIPCHK(c, run_chains(c, x0, x1, R, by_key, cd));
   }
   std::vector<unsigned long long> h(kCountsWords);
   HIPCHK(c, hipMemcpyAsync(h.data(), c->d_counts, kCountsWords * 8, hipMemcpyDeviceToHost, c->stream));

@@ -317,6 +317,136 @@ __global__ __launch_bounds__(256) void k_chains(StreamView sv, int64_t x0, int64
   }
 }
 
+// ---- chain pass, list form ------------------------------------------------------------------------------------
+// Nearly every PASS0 position is a true record start whose successor (p + 4 + block_size) is the next PASS0
+// position.  So the PASS0 positions are listed in order (popcount, scan, write), each gets a link bit
+// ok[i] = "the next record of p_i, by walk_chain's cursor rule, is p_{i+1}, past p_i's name and CIGAR", and
+// p_i's call is Success as soon as ok[i .. i+R-2] all hold: every hop of its chain lands on a PASS0 position,
+// which walk_chain would take through the fast path.  Every other PASS0 position (a link missing within R-1
+// hops: the stream end, a shard edge, a false-positive record start in between, a skip past the name/CIGAR)
+// is walked by walk_chain itself.  Same calls and counts as k_chains; 3 streaming passes instead of R hops per
+// position.
+__global__ __launch_bounds__(256) void k_p0_count(const unsigned long long *__restrict__ bitmap, int64_t nwords,
+                                                  int32_t *__restrict__ chunk_cnt) {
+  const int64_t w0 = (int64_t)blockIdx.x * kChainWords + (int64_t)threadIdx.x * kChainWordsPerThread;
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < kChainWordsPerThread; j++) c += w0 + j < nwords ? (uint32_t)__popcll(bitmap[w0 + j]) : 0u;
+  c = wave_sum(c);
+  __shared__ uint32_t s_c[4];
+  if (lane_id() == 0) s_c[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) chunk_cnt[blockIdx.x] = (int32_t)(s_c[0] + s_c[1] + s_c[2] + s_c[3]);
+}
+
+// exclusive scan of the chunk counts (one workgroup): off[ch], and off[n] = total
+__global__ __launch_bounds__(1024) void k_p0_scan(const int32_t *__restrict__ cnt, int64_t n, int64_t *__restrict__ off) {
+  __shared__ int64_t s_w[16];
+  __shared__ int64_t s_carry;
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  for (int64_t b = 0; b < n; b += 1024) {
+    const int64_t i = b + threadIdx.x;
+    const int64_t v = i < n ? cnt[i] : 0;
+    int64_t incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_w[wv] = incl;
+    __syncthreads();
+    int64_t before = s_carry;
+    for (int k = 0; k < wv; k++) before += s_w[k];
+    if (i < n) off[i] = before + incl - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) s_carry = before + incl;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) off[n] = s_carry;
+}
+
+__global__ __launch_bounds__(256) void k_p0_list(const unsigned long long *__restrict__ bitmap, int64_t nwords,
+                                                 int64_t x0a, const int64_t *__restrict__ chunk_off,
+                                                 int64_t *__restrict__ list) {
+  const int64_t w0 = (int64_t)blockIdx.x * kChainWords + (int64_t)threadIdx.x * kChainWordsPerThread;
+  unsigned long long cw[kChainWordsPerThread];
+  uint32_t mine = 0;
+#pragma unroll
+  for (int j = 0; j < kChainWordsPerThread; j++) {
+    cw[j] = w0 + j < nwords ? bitmap[w0 + j] : 0ull;
+    mine += (uint32_t)__popcll(cw[j]);
+  }
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  uint32_t incl = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  __shared__ uint32_t s_w[4];
+  if (lane == 63) s_w[wv] = incl;
+  __syncthreads();
+  uint32_t before = 0;
+  for (int k = 0; k < wv; k++) before += s_w[k];
+  int64_t idx = chunk_off[blockIdx.x] + before + incl - mine;
+#pragma unroll
+  for (int j = 0; j < kChainWordsPerThread; j++)
+    for (unsigned long long m = cw[j]; m; m &= m - 1) list[idx++] = x0a + ((w0 + j) << 6) + __builtin_ctzll(m);
+}
+
+__global__ __launch_bounds__(256) void k_p0_links(StreamView sv, const int64_t *__restrict__ list,
+                                                  const int64_t *__restrict__ n_ptr, uint8_t *__restrict__ ok) {
+  const int64_t n = *n_ptr;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = list[i];
+    const int32_t bs = g_i32(sv.u, p);
+    const int32_t lrn = sv.u[p + 12];
+    const int32_t nc = (int32_t)((uint32_t)sv.u[p + 16] | ((uint32_t)sv.u[p + 17] << 8));
+    const int64_t c_end = p + 36 + (lrn >= 2 ? lrn : 0) + 4 * (int64_t)nc;
+    const int64_t nxt = p + 4 + (int64_t)bs;
+    ok[i] = (i + 1 < n && list[i + 1] == nxt && nxt > c_end) ? 1 : 0;
+  }
+}
+
+// Success when the R-1 links from p_i hold; every other PASS0 position goes to the fallback list.
+__global__ __launch_bounds__(256) void k_p0_fast(const int64_t *__restrict__ list, const int64_t *__restrict__ n_ptr,
+                                                 const uint8_t *__restrict__ ok, int R, CountsDev cd,
+                                                 int64_t *__restrict__ fb, unsigned long long *__restrict__ n_fb) {
+  const int64_t n = *n_ptr;
+  uint32_t n_succ = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    bool succ = i + (R - 1) <= n - 1 || R <= 1;
+    for (int k = 0; succ && k < R - 1; k++) succ = ok[i + k] != 0;
+    if (succ) n_succ++;
+    else fb[atomicAdd(n_fb, 1ull)] = list[i];
+  }
+  if (cd.counts) {
+    n_succ = wave_sum(n_succ);
+    if (lane_id() == 0 && n_succ) atomicAdd(&cd.scalars[1], (unsigned long long)n_succ);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_p0_fallback(StreamView sv, int64_t x0a, int64_t x1, int R,
+                                                     unsigned long long *__restrict__ bitmap, CountsDev cd, int bykey,
+                                                     const int64_t *__restrict__ fb,
+                                                     const unsigned long long *__restrict__ n_fb) {
+  const int64_t n = (int64_t)*n_fb;
+  uint32_t n_succ = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = fb[i];
+    const uint32_t w = walk_chain(sv, bitmap, x0a, x1, p, R);
+    if (w & W_SUCC) n_succ++;
+    else atomicAnd(&bitmap[(p - x0a) >> 6], ~(1ull << ((p - x0a) & 63)));
+    if (cd.counts) count_chain_result(cd, w, bykey != 0);
+  }
+  if (cd.counts) {
+    n_succ = wave_sum(n_succ);
+    if (lane_id() == 0 && n_succ) atomicAdd(&cd.scalars[1], (unsigned long long)n_succ);
+  }
+}
+
 // ---- first record against the LDS window --------------------------------------------------------------------
 // Global (address space 1) view of the stream: pointers that arrive inside a kernel-argument struct are generic,
 // and generic (flat) loads make every later LDS wait also wait for them.
@@ -866,6 +996,31 @@ hipError_t launch_check_full_chains(StreamView sv, int64_t x0, int64_t x1, int32
                                     unsigned long long *bitmap, hipStream_t s) {
   if (x1 <= x0) return hipSuccess;
   hipLaunchKernelGGL(k_chains, dim3(chain_grid(x0, x1)), dim3(256), 0, s, sv, x0, x1, R, bitmap, cd, by_key, nullptr);
+  return hipGetLastError();
+}
+int64_t chain_list_chunks(int64_t x0, int64_t x1) {
+  const int64_t words = (x1 - (x0 & ~(int64_t)63) + 63) >> 6;
+  return (words + kChainWords - 1) / kChainWords;
+}
+hipError_t launch_chain_list_build(int64_t x0, int64_t x1, const unsigned long long *bitmap, const ChainScratch &cs,
+                                   hipStream_t s) {
+  const int64_t x0a = x0 & ~(int64_t)63, nwords = (x1 - x0a + 63) >> 6, nch = chain_list_chunks(x0, x1);
+  if (nch <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_p0_count, dim3((unsigned)nch), dim3(256), 0, s, bitmap, nwords, cs.chunk_cnt);
+  hipLaunchKernelGGL(k_p0_scan, dim3(1), dim3(1024), 0, s, cs.chunk_cnt, nch, cs.chunk_off);
+  return hipGetLastError();
+}
+hipError_t launch_chain_list_run(StreamView sv, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,
+                                 unsigned long long *bitmap, const ChainScratch &cs, hipStream_t s) {
+  const int64_t x0a = x0 & ~(int64_t)63, nwords = (x1 - x0a + 63) >> 6, nch = chain_list_chunks(x0, x1);
+  if (nch <= 0) return hipSuccess;
+  const int64_t *n_ptr = cs.chunk_off + nch;
+  hipLaunchKernelGGL(k_p0_list, dim3((unsigned)nch), dim3(256), 0, s, bitmap, nwords, x0a, cs.chunk_off, cs.list);
+  hipLaunchKernelGGL(k_p0_links, dim3(4096), dim3(256), 0, s, sv, cs.list, n_ptr, cs.ok);
+  (void)hipMemsetAsync(cs.n_fb, 0, sizeof(unsigned long long), s);
+  hipLaunchKernelGGL(k_p0_fast, dim3(4096), dim3(256), 0, s, cs.list, n_ptr, cs.ok, (int)R, cd, cs.fb, cs.n_fb);
+  hipLaunchKernelGGL(k_p0_fallback, dim3(1024), dim3(256), 0, s, sv, x0a, x1, (int)R, bitmap, cd, (int)by_key, cs.fb,
+                     cs.n_fb);
   return hipGetLastError();
 }
 hipError_t launch_check_eager(StreamView sv, int64_t x0, int64_t x1, int32_t R, unsigned long long *bitmap,

@@ -89,6 +89,20 @@ hipError_t launch_check_full_counts(StreamView sv, int64_t x0, int64_t x1, int32
 // (launch_check_full_counts runs the record-0 pass; launch_check_full_chains then resolves the PASS0 chains)
 hipError_t launch_check_full_chains(StreamView sv, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,
                                     unsigned long long *bitmap, hipStream_t s);
+// list-form chain pass (sbam_check.hip): scratch owned by the context
+struct ChainScratch {
+  int32_t *chunk_cnt;             // [nchunks]
+  int64_t *chunk_off;             // [nchunks + 1]; [nchunks] = number of PASS0 positions
+  int64_t *list;                  // PASS0 positions in order
+  uint8_t *ok;                    // link bits
+  int64_t *fb;                    // fallback positions
+  unsigned long long *n_fb;       // fallback count
+};
+int64_t chain_list_chunks(int64_t x0, int64_t x1);
+hipError_t launch_chain_list_build(int64_t x0, int64_t x1, const unsigned long long *bitmap, const ChainScratch &cs,
+                                   hipStream_t s);
+hipError_t launch_chain_list_run(StreamView sv, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,
+                                 unsigned long long *bitmap, const ChainScratch &cs, hipStream_t s);
 hipError_t launch_check_eager(StreamView sv, int64_t x0, int64_t x1, int32_t R, unsigned long long *bitmap,
                               hipStream_t s);
 hipError_t launch_check_words(StreamView sv, int64_t x0, int64_t x1, int32_t R, uint32_t *words,
