@@ -664,6 +664,8 @@ static int check_range_args(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R) {
   return SBAM_OK;
 }
 
+static hipError_t run_chains(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd);
+
 int sbam_check_eager(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, uint64_t *bitmap) {
   if (!c) return SBAM_ERR_ARG;
   int rc = check_range_args(c, x0, x1, R);
@@ -673,7 +675,8 @@ int sbam_check_eager(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, uint64_t *b
   if (rc) return rc;
   {
     Timer t(c, "check_eager");
-    HIPCHK(c, launch_check_eager(view(c), x0, x1, R, c->d_bitmap, c->stream));
+    HIPCHK(c, launch_check_eager_pass0(view(c), x0, x1, R, c->d_bitmap, c->stream));
+    HIPCHK(c, run_chains(c, x0, x1, R, 0, CountsDev{}));
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (bitmap) {

@@ -1023,12 +1023,11 @@ hipError_t launch_chain_list_run(StreamView sv, int64_t x0, int64_t x1, int32_t 
                      cs.n_fb);
   return hipGetLastError();
 }
-hipError_t launch_check_eager(StreamView sv, int64_t x0, int64_t x1, int32_t R, unsigned long long *bitmap,
-                              hipStream_t s) {
+hipError_t launch_check_eager_pass0(StreamView sv, int64_t x0, int64_t x1, int32_t R, unsigned long long *bitmap,
+                                    hipStream_t s) {
   if (x1 <= x0) return hipSuccess;
   hipLaunchKernelGGL(k_check<MODE_EAGER>, dim3(check_grid(ntiles_of(x0, x1))), dim3(kCheckThreads), 0, s, sv, x0, x1,
                      R, CountsDev{}, bitmap, nullptr);
-  hipLaunchKernelGGL(k_chains, dim3(chain_grid(x0, x1)), dim3(256), 0, s, sv, x0, x1, R, bitmap, CountsDev{}, 0, nullptr);
   return hipGetLastError();
 }
 hipError_t launch_check_words(StreamView sv, int64_t x0, int64_t x1, int32_t R, uint32_t *words,

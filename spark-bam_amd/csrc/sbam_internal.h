@@ -103,8 +103,8 @@ hipError_t launch_chain_list_build(int64_t x0, int64_t x1, const unsigned long l
                                    hipStream_t s);
 hipError_t launch_chain_list_run(StreamView sv, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,
                                  unsigned long long *bitmap, const ChainScratch &cs, hipStream_t s);
-hipError_t launch_check_eager(StreamView sv, int64_t x0, int64_t x1, int32_t R, unsigned long long *bitmap,
-                              hipStream_t s);
+hipError_t launch_check_eager_pass0(StreamView sv, int64_t x0, int64_t x1, int32_t R, unsigned long long *bitmap,
+                                    hipStream_t s);
 hipError_t launch_check_words(StreamView sv, int64_t x0, int64_t x1, int32_t R, uint32_t *words,
                               unsigned long long *bitmap, hipStream_t s);
 hipError_t launch_find_record_starts(StreamView sv, const int64_t *x0, int64_t n, int32_t R, int64_t max_read_size,
