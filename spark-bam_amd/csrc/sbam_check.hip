@@ -22,6 +22,12 @@
 #ifndef SBAM_ABLATE
 #define SBAM_ABLATE 0
 #endif
+#ifndef SBAM_CHECK_WGS  // k_check workgroups per CU the register budget is sized for (launch bounds)
+#define SBAM_CHECK_WGS 4
+#endif
+#ifndef SBAM_CHECK_WGS_INT  // the same for the interior-tiles-only instantiation
+#define SBAM_CHECK_WGS_INT 5
+#endif
 
 namespace sbam {
 
@@ -729,10 +735,12 @@ SB_DEV void bykey_count(uint32_t *s_cnt, int lane, bool counted, uint32_t key, u
   }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(kCheckThreads, 4) void k_check(StreamView sv, int64_t x0, int64_t x1, int R, CountsDev cd,
-                                                         unsigned long long *__restrict__ bitmap,
-                                                         uint32_t *__restrict__ words) {
+// PART 0: every tile of [x0, x1); PART 1: only the interior tiles [tlo, thi) (interior_tiles), compiled without
+// the boundary path so its register budget is its own; PART 2: every tile except [tlo, thi).
+template <int MODE, int PART>
+__global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBAM_CHECK_WGS) void k_check(
+    StreamView sv, int64_t x0, int64_t x1, int R, CountsDev cd, unsigned long long *__restrict__ bitmap,
+    uint32_t *__restrict__ words, int64_t tlo, int64_t thi) {
   constexpr bool EAGER = MODE == MODE_EAGER;
   constexpr bool COUNTS = MODE == MODE_COUNTS || MODE == MODE_BYKEY;
   constexpr bool BYKEY = MODE == MODE_BYKEY;
@@ -762,7 +770,10 @@ __global__ __launch_bounds__(kCheckThreads, 4) void k_check(StreamView sv, int64
   acc.clear();
   int since_flush = 0;
 
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  const int64_t nskip = PART == 2 ? thi - tlo : 0;
+  const int64_t tcount = PART == 1 ? thi - tlo : ntiles - nskip;
+  for (int64_t ti = blockIdx.x; ti < tcount; ti += gridDim.x) {
+    const int64_t t = PART == 1 ? tlo + ti : (ti >= tlo ? ti + nskip : ti);
     const int64_t base = x0a + t * kTile;
     __syncthreads();
     {  // stage the window (32 B per lane per step) and build the op-class and name-character bitmaps
@@ -854,9 +865,13 @@ __global__ __launch_bounds__(kCheckThreads, 4) void k_check(StreamView sv, int64
       add4(acc.pl, Fo);
     }
     };
-    if (base >= x0 && base + kTile <= x1 && base + kTile + kInteriorTail <= sv.L)
+    if constexpr (PART == 1) {
       run_tile(std::integral_constant<bool, true>{});
-    else run_tile(std::integral_constant<bool, false>{});
+    } else {
+      if (base >= x0 && base + kTile <= x1 && base + kTile + kInteriorTail <= sv.L)
+        run_tile(std::integral_constant<bool, true>{});
+      else run_tile(std::integral_constant<bool, false>{});
+    }
     if (COUNTS) {
       if (++since_flush == kFlushTiles) {
         flush_acc(acc, s_acc, lane);
@@ -976,6 +991,28 @@ __global__ void k_record_offsets(StreamView sv, int64_t x, int64_t end, int64_t 
 // ---- launch wrappers ---------------------------------------------------------------------------------------
 static int check_grid(int64_t ntiles) { return (int)(ntiles < 1 ? 1 : ntiles > 2048 ? 2048 : ntiles); }
 static int64_t ntiles_of(int64_t x0, int64_t x1) { return (x1 - (x0 & ~(int64_t)63) + kTile - 1) / kTile; }
+// Tiles [tlo, thi) of [x0, x1) are interior (inside [x0, x1), ending >= kInteriorTail bytes before the stream end).
+static void interior_tiles(const StreamView &sv, int64_t x0, int64_t x1, int64_t *tlo, int64_t *thi) {
+  const int64_t x0a = x0 & ~(int64_t)63;
+  const int64_t lim = x1 < sv.L - kInteriorTail ? x1 : sv.L - kInteriorTail;
+  *tlo = x0 == x0a ? 0 : 1;
+  *thi = lim - x0a >= kTile ? (lim - x0a) / kTile : 0;
+  if (*thi < *tlo) *thi = *tlo;
+}
+// Record-0 pass of mode MODE over [x0, x1): interior tiles by k_check<MODE, 1>, the rest by k_check<MODE, 2>.
+template <int MODE>
+static void launch_split_check(StreamView sv, int64_t x0, int64_t x1, int32_t R, CountsDev cd,
+                               unsigned long long *bitmap, hipStream_t s) {
+  int64_t tlo, thi;
+  interior_tiles(sv, x0, x1, &tlo, &thi);
+  const int64_t nt = ntiles_of(x0, x1), ni = thi - tlo;
+  if (ni > 0)
+    hipLaunchKernelGGL((k_check<MODE, 1>), dim3(check_grid(ni)), dim3(kCheckThreads), 0, s, sv, x0, x1, R, cd, bitmap,
+                       nullptr, tlo, thi);
+  if (nt > ni)
+    hipLaunchKernelGGL((k_check<MODE, 2>), dim3(check_grid(nt - ni)), dim3(kCheckThreads), 0, s, sv, x0, x1, R, cd,
+                       bitmap, nullptr, tlo, thi);
+}
 static int chain_grid(int64_t x0, int64_t x1) {
   const int64_t words = (x1 - (x0 & ~(int64_t)63) + 63) >> 6;
   const int64_t g = (words + kChainWords - 1) / kChainWords;
@@ -985,11 +1022,11 @@ static int chain_grid(int64_t x0, int64_t x1) {
 hipError_t launch_check_full_counts(StreamView sv, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,
                                     unsigned long long *bitmap, hipStream_t s) {
   if (x1 <= x0) return hipSuccess;
-  const int g = check_grid(ntiles_of(x0, x1));
   if (by_key)
-    hipLaunchKernelGGL(k_check<MODE_BYKEY>, dim3(g), dim3(kCheckThreads), 0, s, sv, x0, x1, R, cd, bitmap, nullptr);
+    hipLaunchKernelGGL((k_check<MODE_BYKEY, 0>), dim3(check_grid(ntiles_of(x0, x1))), dim3(kCheckThreads), 0, s, sv,
+                       x0, x1, R, cd, bitmap, nullptr, (int64_t)0, (int64_t)0);
   else
-    hipLaunchKernelGGL(k_check<MODE_COUNTS>, dim3(g), dim3(kCheckThreads), 0, s, sv, x0, x1, R, cd, bitmap, nullptr);
+    launch_split_check<MODE_COUNTS>(sv, x0, x1, R, cd, bitmap, s);
   return hipGetLastError();
 }
 hipError_t launch_check_full_chains(StreamView sv, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,
@@ -1026,15 +1063,14 @@ hipError_t launch_chain_list_run(StreamView sv, int64_t x0, int64_t x1, int32_t 
 hipError_t launch_check_eager_pass0(StreamView sv, int64_t x0, int64_t x1, int32_t R, unsigned long long *bitmap,
                                     hipStream_t s) {
   if (x1 <= x0) return hipSuccess;
-  hipLaunchKernelGGL(k_check<MODE_EAGER>, dim3(check_grid(ntiles_of(x0, x1))), dim3(kCheckThreads), 0, s, sv, x0, x1,
-                     R, CountsDev{}, bitmap, nullptr);
+  launch_split_check<MODE_EAGER>(sv, x0, x1, R, CountsDev{}, bitmap, s);
   return hipGetLastError();
 }
 hipError_t launch_check_words(StreamView sv, int64_t x0, int64_t x1, int32_t R, uint32_t *words,
                               unsigned long long *bitmap, hipStream_t s) {
   if (x1 <= x0) return hipSuccess;
-  hipLaunchKernelGGL(k_check<MODE_WORDS>, dim3(check_grid(ntiles_of(x0, x1))), dim3(kCheckThreads), 0, s, sv, x0, x1,
-                     R, CountsDev{}, bitmap, words);
+  hipLaunchKernelGGL((k_check<MODE_WORDS, 0>), dim3(check_grid(ntiles_of(x0, x1))), dim3(kCheckThreads), 0, s, sv, x0,
+                     x1, R, CountsDev{}, bitmap, words, (int64_t)0, (int64_t)0);
   hipLaunchKernelGGL(k_chains, dim3(chain_grid(x0, x1)), dim3(256), 0, s, sv, x0, x1, R, bitmap, CountsDev{}, 0, words);
   return hipGetLastError();
 }
