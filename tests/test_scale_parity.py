@@ -1,7 +1,8 @@
 """configs[2]-style verdict diff at scale: on a multi-GB synthetic BAM resident on the GPU, the full checker's
 result word at every offset of randomly sampled block runs equals the CPU oracle's, the oracle inflating those
-blocks itself from the compressed bytes (an independent stream).  The bench's full-size properties (records ==
-checker calls == generator count) cover the rest of the file.  SBAM_SCALE_GB sets the size (default 4)."""
+blocks itself from the compressed bytes (an independent stream); 4096 sampled blocks inflate to the CRC32 and
+ISIZE their BGZF footers store; and the eager and full checks agree at every offset and call exactly the
+generated records.  SBAM_SCALE_GB sets the size (default 4)."""
 import os
 
 import numpy as np
@@ -36,3 +37,16 @@ def test_sampled_verdicts_at_scale():
             assert bad.size == 0, (b, bad[:5], got[bad[:5]], want[bad[:5]])
             compared += x1
         assert compared > 48 * 8 * 60000
+        # inflate at scale: each sampled block's bytes match the CRC32 its BGZF footer stores (the reference never
+        # checks it, but a correct inflate reproduces it), and its size the footer's ISIZE
+        import zlib
+        for b in np.sort(rng.choice(st.size, 4096, replace=False)).tolist():
+            end = int(st[b]) + int(cs[b])
+            crc, isize = (int.from_bytes(data[end - 8 + k:end - 4 + k].tobytes(), "little") for k in (0, 4))
+            raw = g.read_uncompressed(int(uo[b]), int(us[b]))
+            assert len(raw) == isize and zlib.crc32(raw) == crc, b
+        # eager and full checks agree at every offset, and call exactly the generated records
+        L = g.uncompressed_size
+        eager = g.check_eager(0, L)
+        c, full = g.check_full_counts(0, L, want_bitmap=True)
+        assert np.array_equal(eager, full) and int(eager.sum()) == c.n_success == s.n_records
