@@ -99,6 +99,25 @@ SB_DEV int canon_decode(const Canon &c, uint64_t bb, int &len, bool &valid, int 
   return valid ? (int)(rev >> (15 - L)) + (p >> 14) : 0;
 }
 
+// canon_decode over a per-lane choice of alphabet (b when useB): the second symbol slot of a step decodes a
+// distance after a length and another literal/length after a literal, in one instruction stream.
+SB_DEV int canon_decode_sel(const Canon &a, const Canon &b, bool useB, uint64_t bb, int &len, bool &valid,
+                            int &hist) {
+  const uint32_t rev = __builtin_bitreverse32((uint32_t)bb) >> 17;
+  int32_t p = useB ? b.pk[1] : a.pk[1];
+  sfor<1, 15>([&](auto I) {
+    constexpr int l = decltype(I)::value;
+    const uint32_t lim = useB ? b.lim[l] : a.lim[l];
+    const int32_t pn = useB ? b.pk[l + 1] : a.pk[l + 1];
+    p = rev >= lim ? pn : p;
+  });
+  const int L = p & 31;
+  valid = rev < (useB ? b.lim[15] : a.lim[15]);
+  len = valid ? L : 1;
+  hist = (p >> 5) & 511;
+  return valid ? (int)(rev >> (15 - L)) + (p >> 14) : 0;
+}
+
 // 15 counters of 9 bits (code lengths 1..15) in three u64: fields 0-6, 7-13, 14-15.
 struct Cnt15 {
   uint64_t a = 0, b = 0, c = 0;
@@ -601,6 +620,8 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
         state = S_DONE;
       } else {
         br.drop(L1);
+        int len = 0;
+        bool is_len = false;
         if (sym < 256) {
           if (!tok_put(to, (uint32_t)sym, pool, pool_next, npages)) err = INF_OVERFLOW;
           o++;
@@ -620,13 +641,28 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
             err = INF_SHORT;
             state = S_DONE;
           } else {
-            const int len = lb + (int)br.peek(lx);
+            len = lb + (int)br.peek(lx);
             br.drop(lx);
-            refill();
-            int L2, h2;
-            bool v2;
-            const int i2 = canon_decode(dc, br.bb, L2, v2, h2);
-            const int ds = *sl.b(kDistSorted + i2);
+            is_len = true;
+          }
+        }
+        // second slot: the distance after a length, or a second literal after a literal (taken only when it
+        // is a complete, valid literal; anything else is left for the next step, which decodes it afresh)
+        if (is_len || (sym < 256 && state == S_HUFF)) {
+          refill();
+          int L2, h2;
+          bool v2;
+          const int i2 = canon_decode_sel(lc, dc, is_len, br.bb, L2, v2, h2);
+          const int b2 = *sl.b((is_len ? kDistSorted : kLitSorted) + i2);
+          if (!is_len) {
+            if (v2 && i2 < h2 && br.left >= L2) {
+              br.drop(L2);
+              if (!tok_put(to, (uint32_t)b2, pool, pool_next, npages)) err = INF_OVERFLOW;
+              o++;
+              if (o == us || err != INF_OK) state = S_DONE;
+            }
+          } else {
+            const int ds = b2;
             if (br.left < L2) {
               err = INF_SHORT;
               state = S_DONE;
