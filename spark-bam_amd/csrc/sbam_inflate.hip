@@ -378,8 +378,10 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
         }
       }
     }
-    if (__all(state == S_EXIT)) break;
-    {  // release parked lanes together (see kParkMin)
+    // wave-level decisions at epoch steps only (a parked or exited lane idles at most kEpoch - 1 steps)
+    if ((it & (kEpoch - 1)) == 0) {
+      if (__all(state == S_EXIT)) break;
+      // release parked lanes together (see kParkMin)
       const uint64_t pk = __ballot(state == S_PARK);
       const uint64_t dc = __ballot(state == S_HUFF || state == S_STORED);
       if (pk && (__popcll(pk) >= kParkMin || dc == 0) && state == S_PARK) state = S_HDR;
