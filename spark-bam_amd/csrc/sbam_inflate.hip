@@ -765,42 +765,51 @@ constexpr int kResRing = 136;  // per-lane ring stride (128 B used): 34 dwords, 
 // by < 64 B when a copy starts, so a source 80 B back is stored; the ring still holds 105 B behind the output.
 constexpr int kNear = 80;
 
+// Tokens are read a group of kTokGroupChunks 16-B chunks at a time (aligned; a page's first group starts with
+// the next-page link).
+#ifndef SBAM_TOK_GROUP
+#define SBAM_TOK_GROUP 128
+#endif
+constexpr int kTG = SBAM_TOK_GROUP / 16;  // chunks per token group
+static_assert(kTG >= 2 && (kTokPage % SBAM_TOK_GROUP) == 0, "token groups tile a page");
+
 struct TokIn {
-  uint32_t t0, t1, t2, t3;  // current chunk (t0 low half = next token)
-  uint32_t q[12];           // up to three more chunks
-  int n;                    // tokens left in t0..t3
-  int nq;                   // chunks left in q
-  uint64_t cur;             // byte offset of the next 64-B group in the pool
-  uint32_t pnext;           // next page of this block
+  uint32_t t0, t1, t2, t3;      // current chunk (t0 low half = next token)
+  uint32_t q[4 * (kTG - 1)];    // up to kTG - 1 more chunks
+  int n;                        // tokens left in t0..t3
+  int nq;                       // chunks left in q
+  uint64_t cur;                 // byte offset of the next group in the pool
+  uint32_t pnext;               // next page of this block
   SB_DEV void load(const uint8_t *pool) {
     const uint4 *g = reinterpret_cast<const uint4 *>(pool + cur);
-    const uint4 a = g[0], b = g[1], c = g[2], d = g[3];
-    if ((cur & (kTokPage - 1)) == 0) {  // a page's first group: chunk 0 links to the next page
-      pnext = a.x;
-      q[0] = b.x; q[1] = b.y; q[2] = b.z; q[3] = b.w;
-      q[4] = c.x; q[5] = c.y; q[6] = c.z; q[7] = c.w;
-      q[8] = d.x; q[9] = d.y; q[10] = d.z; q[11] = d.w;
-      t0 = t1 = t2 = t3 = 0;
-      nq = 3;
-    } else {
-      t0 = a.x; t1 = a.y; t2 = a.z; t3 = a.w;
-      q[0] = b.x; q[1] = b.y; q[2] = b.z; q[3] = b.w;
-      q[4] = c.x; q[5] = c.y; q[6] = c.z; q[7] = c.w;
-      q[8] = d.x; q[9] = d.y; q[10] = d.z; q[11] = d.w;
-      nq = 4;  // (t counts as the first)
+    uint4 c[kTG];
+#pragma unroll
+    for (int k = 0; k < kTG; k++) c[k] = g[k];
+#pragma unroll
+    for (int k = 1; k < kTG; k++) {
+      q[4 * (k - 1) + 0] = c[k].x; q[4 * (k - 1) + 1] = c[k].y;
+      q[4 * (k - 1) + 2] = c[k].z; q[4 * (k - 1) + 3] = c[k].w;
     }
-    cur += 64;
+    if ((cur & (kTokPage - 1)) == 0) {  // a page's first group: chunk 0 links to the next page
+      pnext = c[0].x;
+      t0 = t1 = t2 = t3 = 0;
+      nq = kTG - 1;
+    } else {
+      t0 = c[0].x; t1 = c[0].y; t2 = c[0].z; t3 = c[0].w;
+      nq = kTG;  // (t counts as the first)
+    }
+    cur += 16 * kTG;
     if ((cur & (kTokPage - 1)) == 0) cur = (uint64_t)pnext * kTokPage;
   }
   SB_DEV uint32_t get(const uint8_t *pool) {
     if (n == 0) {
       if (nq == 0) load(pool);
-      if (nq == 4) {
-        nq = 3;
+      if (nq == kTG) {
+        nq = kTG - 1;
       } else {
         t0 = q[0]; t1 = q[1]; t2 = q[2]; t3 = q[3];
 #pragma unroll
-        for (int k = 0; k < 8; k++) q[k] = q[k + 4];
+        for (int k = 0; k < 4 * (kTG - 2); k++) q[k] = q[k + 4];
         nq--;
       }
       n = 8;
