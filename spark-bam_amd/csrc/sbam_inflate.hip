@@ -764,6 +764,12 @@ constexpr int kResRing = 136;  // per-lane ring stride (128 B used): 34 dwords, 
 // Copies with (effective) distance <= kNear read the ring, longer ones HBM.  The flushed mark trails the output
 // by < 64 B when a copy starts, so a source 80 B back is stored; the ring still holds 105 B behind the output.
 constexpr int kNear = 80;
+// Literals a step may take (the first token plus up to kResLits - 1 more literals already in the current chunk).
+#ifndef SBAM_RES_LITS
+#define SBAM_RES_LITS 4
+#endif
+constexpr int kResLits = SBAM_RES_LITS;
+static_assert(kResLits >= 1 && kResLits <= 8, "a step writes at most 16 ring bytes");
 
 // Tokens are read a group of kTokGroupChunks 16-B chunks at a time (aligned; a page's first group starts with
 // the next-page link).
@@ -840,7 +846,7 @@ __global__ __launch_bounds__(kResThreads, 4) void k_inflate_resolve(BlockTable b
   TokIn ti;
   ti.t0 = ti.t1 = ti.t2 = ti.t3 = 0;
 #pragma unroll
-  for (int k = 0; k < 12; k++) ti.q[k] = 0;
+  for (int k = 0; k < 4 * (kTG - 1); k++) ti.q[k] = 0;
   ti.n = ti.nq = 0;
   ti.cur = 0;
   ti.pnext = 0;
@@ -879,6 +885,15 @@ __global__ __launch_bounds__(kResThreads, 4) void k_inflate_resolve(BlockTable b
       if (t < 256) {
         ring[a & 127] = (uint8_t)t;
         a++;
+        // more literals of a run, up to kResLits per step, from the current chunk
+#pragma unroll
+        for (int k = 1; k < kResLits; k++) {
+          const uint32_t t2 = ti.t0 & 0xffffu;
+          if (!(ti.n > 0 && t2 < 256 && a < ae)) break;
+          ring[a & 127] = (uint8_t)t2;
+          a++;
+          ti.get(pool);
+        }
       } else if (t != kTokPad) {
         crem = (int)t - 253;
         eff = (int)ti.get(pool) + 1;
