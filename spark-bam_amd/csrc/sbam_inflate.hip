@@ -938,6 +938,16 @@ __global__ __launch_bounds__(kResThreads, 4) void k_inflate_resolve(BlockTable b
       crem -= n;
       if (n == eff && eff < 16) eff *= 2;  // the copied bytes extend the period: distance 2·eff is valid
     }
+    if (crem == 0) {  // literals that follow the copy (or the step's literals), from the current chunk
+#pragma unroll
+      for (int k = 1; k < kResLits; k++) {
+        const uint32_t t2 = ti.t0 & 0xffffu;
+        if (!(ti.n > 0 && t2 < 256 && a < ae)) break;
+        ring[a & 127] = (uint8_t)t2;
+        a++;
+        ti.get(pool);
+      }
+    }
     // flush: a block's partial first chunk (shared with the previous block) as bytes, then aligned 16-B
     // chunks up to a 64-B boundary, then whole 64-B groups
     if (fl & 15) {
