@@ -14,10 +14,11 @@
 //     The symbol stream leaves as u16 tokens in 4 KiB pages of an HBM pool (16-B stores; lanes grab pages
 //     with an atomic counter).  No lane ever reads the output, so this kernel never waits on HBM except
 //     for its (prefetched) input dwords.
-//   k_inflate_resolve — one lane per BGZF block again, but with no tables: 2048 lanes per CU hide the
-//     latency of back-reference loads.  Tokens become bytes in a 64-B per-lane LDS ring that leaves as
-//     aligned 16-B stores; copies with distance <= 40 read the ring, longer ones read HBM (4-B aligned
-//     loads + v_alignbyte).  Overlapping copies double their distance per step (the period stays valid).
+//   k_inflate_resolve — one lane per BGZF block again, but with no tables: 1024 lanes per CU hide the
+//     latency of back-reference loads.  Tokens become bytes in a 128-B per-lane LDS ring that leaves as
+//     aligned 64-B groups; copies with distance <= kNear read the ring, longer ones are one unaligned 16-B
+//     load from the output already stored.  A step takes a token plus the literals that follow it (or follow
+//     the copy) in the current chunk.  Overlapping copies double their distance per step.
 #include <type_traits>
 
 #include "sbam_internal.h"
@@ -757,7 +758,7 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
 // ---- resolve kernel -------------------------------------------------------------------------------------------
 // One lane per BGZF block.  Both of its HBM streams are shaped for the memory side, which bounds this kernel:
 // with every block in flight, a lane's share of L2 is tens of bytes, so a 16-B access to a line costs the whole
-// line.  Tokens are read 64 B (32 tokens) at a time; output leaves in 64-B aligned groups of four 16-B stores
+// line.  Tokens are read 128 B (64 tokens) at a time; output leaves in 64-B aligned groups of four 16-B stores
 // (the line is written whole while it is still in L2); a far copy is one unaligned 16-B load.
 constexpr int kResThreads = 256;
 constexpr int kResRing = 136;  // per-lane ring stride (128 B used): 34 dwords, 8-B aligned
