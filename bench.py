@@ -11,18 +11,22 @@ resident in HBM:
     → split assembly (+ all_gather of split starts / all_reduce of Counts when N > 1)
 
 N > 1: one process per GPU (torch.distributed, RCCL), rank r owns a contiguous run of Hadoop splits of an
-N × size-gb file (weak scaling) and loads only its byte range + halo (sbam/dist.py).
+N × size-gb file (weak scaling) and loads only its byte range + halo (sbam/dist.py).  `--gpus N` without a
+torchrun environment spawns the N ranks itself (torch.distributed.run) before anything touches the GPU.
 
 Prints ONE JSON line (rank 0).  `roofline` is for the dominant kernel (largest average device time),
-measured with HIP events on the library's stream over the timed steps; `cpu_baseline` times the CPU oracle
-(oracle/, a C restatement of the reference — the Scala/Spark reference cannot run on this image) on a
-bounded sample of the same generator on the host cores.
+measured with HIP events on the library's stream over the timed steps; `e2e_h2d` is the same step from
+pinned host memory (host → device copies inside the timed step, overlapped with the kernels of the previous
+window); `cpu_baseline` times the CPU oracle (oracle/, a C restatement of the reference — the Scala/Spark
+reference cannot run on this image) on a bounded sample of the same generator on the host cores.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -40,12 +44,37 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def spawn_ranks(n: int) -> int:
+    """`bench.py --gpus N` outside torchrun: launch N ranks (one per GPU) with torch.distributed.run and return
+    its exit code.  This process has not imported torch, so no GPU has been touched before the children start."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"[launcher] {' '.join(cmd)}")
+    return subprocess.call(cmd)
+
+
+def host_cores():
+    """(threads the host side may use, CPUs the machine shows).  A GPU box's process gets a share of a larger
+    machine: OMP_NUM_THREADS (16 there) is that share; os.cpu_count() is the whole machine."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (min(aff, share) if share > 0 else aff), (os.cpu_count() or aff)
+
+
 def measured_traffic(kernel: str, args):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes (tools/traffic_pmc.py →
-    profiles/*/traffic.json), when they were taken on this same workload; else None.  FETCH_SIZE is doubled
-    for the kernels' 16-B/lane streaming reads (MI355X_MICROARCH.md, HBM/rocprofv3: gfx950 tallies each
-    128-B request at 64 B); WRITE_SIZE is used as reported."""
+    profiles/*/traffic.json), when they were taken on this same workload AND the same kernel build (the
+    library's source digest); else None.  FETCH_SIZE is doubled for the kernels' 16-B/lane streaming reads
+    (MI355X_MICROARCH.md, HBM/rocprofv3: gfx950 tallies each 128-B request at 64 B); WRITE_SIZE as reported."""
     import glob
+    import sbam
+    digest = sbam.source_digest()
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json")), reverse=True):
         try:
             t = json.load(open(path))
@@ -53,10 +82,36 @@ def measured_traffic(kernel: str, args):
             continue
         if t.get("workload") != {"size_gb": args.size_gb, "seed": args.seed, "tile_mb": args.tile_mb}:
             continue
+        if t.get("source_digest") != digest:
+            continue
         k = t.get("kernels", {}).get(kernel)
         if k:
             return {"hbm_bytes_per_launch": k["hbm_bytes_per_launch"], "source": os.path.relpath(path, ROOT)}
     return None
+
+
+def copy_peak(dev) -> dict:
+    """Measured HBM copy rate on this GPU: a 4 GiB device-to-device tensor copy (read + write bytes / time)."""
+    import torch
+    n = 4 << 30
+    a = torch.empty(n, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1)
+    for _ in range(2):
+        b.copy_(a)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 10
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    torch.cuda.empty_cache()
+    return {"value": round(2 * n / (ms * 1e-3) / 1e9, 1), "unit": "GB/s", "bytes": 2 * n,
+            "how": "torch uint8 copy_ of 4 GiB device->device, read+write bytes / time, 10 reps"}
 
 
 def cpu_baseline(sample_mb: float, threads: int, split_size: int, seed: int):
@@ -79,6 +134,53 @@ def cpu_baseline(sample_mb: float, threads: int, split_size: int, seed: int):
                       f"compute-splits @ {split_size >> 20} MiB, {wall:.2f} s wall"}
 
 
+class WindowPipe:
+    """A rank's byte range streamed through two contexts in W windows: while window w computes on one context, a
+    loader thread makes window w+1's bytes resident in the other (host staging by `stage`, then sbam_load's
+    pinned host → device copy).  A step starts with window 0 loaded in the foreground, so every step is a
+    complete host → results pass."""
+
+    def __init__(self, wplans, stage, split_size, contig_lengths, device, run_window):
+        from concurrent.futures import ThreadPoolExecutor
+        from sbam import dist as sdist
+        self.sdist = sdist
+        self.wplans, self.stage, self.split_size = wplans, stage, split_size
+        self.contig_lengths, self.device, self.run_window = contig_lengths, device, run_window
+        self.loader = ThreadPoolExecutor(max_workers=1)
+        self.ctx = [None, None]
+
+    def _load(self, w, j):
+        wp = self.wplans[w]
+        sh = self.ctx[j]
+        lo, hi = wp.load_range(sh.halo if sh is not None else 2 << 20)
+        buf = self.stage(lo, hi, j)
+        if sh is None:
+            self.ctx[j] = self.sdist.GpuShard(wp, lambda a, b: buf if (a, b) == (lo, hi) else self.stage(a, b, j),
+                                              self.split_size, self.contig_lengths, device=self.device)
+        else:
+            sh.reload(wp, buf)
+        return self.ctx[j]
+
+    def step(self):
+        W = len(self.wplans)
+        out = []
+        fut = None
+        sh = self._load(0, 0)
+        for w in range(W):
+            if w > 0:
+                sh = fut.result()
+            if w + 1 < W:
+                fut = self.loader.submit(self._load, w + 1, (w + 1) % 2)
+            out.append(self.run_window(sh))
+        return out
+
+    def close(self):
+        self.loader.shutdown()
+        for sh in self.ctx:
+            if sh is not None:
+                sh.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -87,10 +189,13 @@ def main():
     ap.add_argument("--size-gb", type=float, default=10.0, help="compressed GB per GPU")
     ap.add_argument("--split-mb", type=float, default=2.0)
     ap.add_argument("--tile-mb", type=float, default=64.0)
-    ap.add_argument("--threads", type=int, default=16, help="host threads (generator, CPU baseline)")
+    ap.add_argument("--threads", type=int, default=0, help="host threads (generator, CPU baseline); 0 = the host share")
     ap.add_argument("--cpu-sample-mb", type=float, default=2000.0,
                     help="compressed MB of the same synthetic file timed on the CPU oracle (~10 s at 16 threads)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e-windows", type=int, default=4,
+                    help="windows of the pinned-host → results measurement (0 = skip it)")
+    ap.add_argument("--e2e-steps", type=int, default=2)
     ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EEDBA11)
     ap.add_argument("--workload", choices=["full-check", "load-reads"], default="full-check",
                     help="full-check: BASELINE metric (compute-splits + full-check); load-reads: configs[3] "
@@ -105,8 +210,16 @@ def main():
     ap.add_argument("--device", type=int, default=None, help="GPU index (default LOCAL_RANK)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
+    if world != args.gpus:
+        log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+        sys.exit(2)
+    threads, nproc = host_cores()
+    if args.threads > 0:
+        threads = args.threads
     local = int(os.environ.get("LOCAL_RANK", 0)) if args.device is None else args.device
     import torch
     torch.cuda.set_device(local)
@@ -128,15 +241,18 @@ def main():
     split_size = int(args.split_mb * (1 << 20))
     t = time.time()
     s = synth.SynthBam.for_size(int(args.size_gb * 1e9 * world), tile_mb=args.tile_mb, seed=args.seed,
-                                threads=args.threads, read_len=args.read_len)
+                                threads=threads, read_len=args.read_len)
     W = max(1, args.windows)
     plans = sdist.plan_shards(s.size, split_size, world)  # rank-level plans (what all_gather sees)
     plan = plans[rank]
-    wplans = sdist.plan_shards(s.size, split_size, world * W)[rank * W:(rank + 1) * W]
+
+    def wplans_of(nw):
+        return sdist.plan_shards(s.size, split_size, world * nw)[rank * nw:(rank + 1) * nw]
+
     shard = sdist.GpuShard(plan, s.slice, split_size, s.contig_lengths, device=local) if W == 1 else None
     log(f"[rank {rank}] synthetic file {s.size / 1e9:.2f} GB ({s.n_records} records), shard "
         f"[{plan.lo}, {plan.owned_hi}) splits {plan.split_first}+{plan.split_count} in {W} window(s), "
-        f"workload {args.workload}, setup {time.time() - t:.1f}s")
+        f"workload {args.workload}, setup {time.time() - t:.1f}s, host threads {threads} of {nproc}")
     kernels = ("scan", "chain", "inflate", "inflate_decode", "inflate_resolve", "check_full", "check_pass0",
                "check_chains", "find_record", "records", "load_records")
     last = {}
@@ -150,68 +266,42 @@ def main():
         else:
             r = sh.step()
         ms = {k: max(sh.f.kernel_ms(k), 0.0) for k in kernels}
-        last.update(U=int(sh.f.uncompressed_size), blocks=sh.f.blocks(), f=sh.f)
-        return r, ms
+        st = sh.f.blocks()
+        return r, ms, int(sh.f.uncompressed_size), st
 
-    # --windows W: a shard larger than HBM streams through two contexts (sbam_load keeps their allocations):
-    # while one computes window w, a loader thread fills pinned host memory with window w+1 (the synthetic
-    # file's slice, copied by `threads` workers) and copies it to the other context's device buffer.
-    loader = fill_pool = None
+    def merge(parts):
+        res = sdist.ShardResult(np.sum([p[0].counts for p in parts], axis=0),
+                                *(np.concatenate([getattr(p[0], a) for p in parts]) for a in
+                                  ("first_block_pos", "first_offset", "nonempty", "n_records")))
+        ms = {k: sum(p[1][k] for p in parts) for k in kernels}
+        last.update(U=sum(p[2] for p in parts), nblocks=sum(p[3][0].size for p in parts),
+                    payload=sum(int(p[3][1].astype(np.int64).sum()) for p in parts))
+        return res, ms
+
+    # --windows W: a shard larger than HBM streams through two contexts; each window's bytes are staged from
+    # the synthetic generator into pinned host memory (16 copy threads) and copied to the device.
+    pipe = None
     if W > 1:
         from concurrent.futures import ThreadPoolExecutor
-        loader, fill_pool = ThreadPoolExecutor(max_workers=1), ThreadPoolExecutor(max_workers=args.threads)
-        wshards, pinned = [None, None], [None, None]
+        fill_pool = ThreadPoolExecutor(max_workers=threads)
+        pinned = [None, None]
 
-        def fill(buf, lo, hi):
-            n, k = hi - lo, args.threads
+        def stage_synth(lo, hi, j):
+            if pinned[j] is None or pinned[j].numel() < hi - lo:
+                pinned[j] = torch.empty(int((hi - lo) * 1.05), dtype=torch.uint8, pin_memory=True)
+            buf = pinned[j].numpy()[:hi - lo]
+            n, k = hi - lo, threads
             step_b = -(-n // k)
             futs = [fill_pool.submit(s.slice, lo + a, lo + min(n, a + step_b), buf[a:min(n, a + step_b)])
                     for a in range(0, n, step_b)]
             for fu in futs:
                 fu.result()
+            return buf
 
-        def load(w, j):  # window w into context slot j (slots alternate per load, so W may be odd)
-            wp = wplans[w]
-            sh = wshards[j]
-            lo, hi = wp.load_range(sh.halo if sh is not None else 2 << 20)
-            if pinned[j] is None or pinned[j].numel() < hi - lo:
-                pinned[j] = torch.empty(int((hi - lo) * 1.05), dtype=torch.uint8, pin_memory=True)
-            buf = pinned[j].numpy()[:hi - lo]
-            fill(buf, lo, hi)
-            if sh is None:
-                wshards[j] = sdist.GpuShard(wp, lambda a, b: buf if (a, b) == (lo, hi) else s.slice(a, b), split_size,
-                                            s.contig_lengths, device=local)
-            else:
-                sh.reload(wp, buf)
-            return wshards[j]
-
-        pending = {"w": 0, "seq": 0, "fut": loader.submit(load, 0, 0)}
+        pipe = WindowPipe(wplans_of(W), stage_synth, split_size, s.contig_lengths, local, run_window)
 
     def step():
-        if W == 1:
-            res, ms = run_window(shard)
-        else:
-            parts, ms = [], {k: 0.0 for k in kernels}
-            U, nb = 0, 0
-            for w in range(W):
-                assert pending["w"] == w
-                sh = pending["fut"].result()
-                nxt = (w + 1) % W  # the next window (of this step or the next one) loads while this one runs
-                pending["seq"] += 1
-                pending.update(w=nxt, fut=loader.submit(load, nxt, pending["seq"] % 2))
-                try:
-                    r, m = run_window(sh)
-                    U += last["U"]
-                    nb += last["blocks"][0].size
-                finally:
-                    last.pop("f", None)
-                parts.append(r)
-                for k in kernels:
-                    ms[k] += m[k]
-            last.update(U=U, nblocks=nb)
-            res = sdist.ShardResult(np.sum([r.counts for r in parts], axis=0),
-                                    *(np.concatenate([getattr(r, a) for r in parts]) for a in
-                                      ("first_block_pos", "first_offset", "nonempty", "n_records")))
+        res, ms = merge([run_window(shard)] if W == 1 else pipe.step())
         if world > 1 and args.workload == "full-check":
             sdist.gather_results(res, plans, device=cdev)
         return res, ms
@@ -220,6 +310,13 @@ def main():
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        tt = torch.tensor([x], dtype=torch.float64, device=cdev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
 
     res = None
     for _ in range(args.warmup):
@@ -234,56 +331,88 @@ def main():
         for k in kernels:
             tot_ms[k] += ms[k]
     sync()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0)
 
     # --- size-independent parity properties of the last step (full sizes; fixtures cover exactness)
     counts = sdist.unpack_counts(res.counts)
     n_rec = int(res.n_records.sum())
     if args.workload == "load-reads":  # no checker pass in this workload: the record count is the property
         counts["n_success"] = n_rec
-    ok_local = counts["n_success"] == int(res.n_records.sum()) if world == 1 else True
+    ok_local = counts["n_success"] == n_rec
     if world > 1:
-        v = torch.tensor([counts["n_success"], n_rec], dtype=torch.int64, device=cdev)
+        v = torch.tensor([counts["n_success"], n_rec, int(not ok_local)], dtype=torch.int64, device=cdev)
         dist.all_reduce(v)
-        tot_succ, tot_rec = (int(x) for x in v.tolist())
+        tot_succ, tot_rec, n_bad = (int(x) for x in v.tolist())
     else:
-        tot_succ, tot_rec = counts["n_success"], n_rec
+        tot_succ, tot_rec, n_bad = counts["n_success"], n_rec, int(not ok_local)
     parity = {"records": tot_rec, "expected_records": s.n_records, "checker_true": tot_succ,
-              "ok": bool(tot_rec == s.n_records and tot_succ == s.n_records and ok_local)}
+              "ok": bool(tot_rec == s.n_records and tot_succ == s.n_records and n_bad == 0)}
     if not parity["ok"]:
         log(f"[rank {rank}] PARITY PROPERTY FAILED: {parity}")
 
     # --- roofline of the dominant kernel (this rank's shard; per launch).  Candidates are single kernels:
-    # k_check<0, 1> (record-0 pass over the interior tiles: reads U, writes the U/8 PASS0 bitmap), k_inflate_decode (reads the C payload;
-    # its token stream is an internal intermediate) and k_inflate_resolve (writes U; tokens internal).
-    U = last["U"]
-    if W == 1:
-        st, cs, us, uo = last["blocks"]
-        comp_payload = int(cs.astype(np.int64).sum())
-        nblocks = int(st.size)
-    else:  # per-window launches; the roofline uses the summed window times and bytes
-        comp_payload = plan.owned_hi - plan.lo
-        nblocks = last["nblocks"]
+    # k_check<0, 1> (record-0 pass over the interior tiles: reads U, writes the U/8 PASS0 bitmap),
+    # k_inflate_decode (reads the C payload; its token stream is an internal intermediate) and
+    # k_inflate_resolve (writes U; tokens internal).
+    U, nblocks, comp_payload = last["U"], last["nblocks"], last["payload"]
     avg = {k: tot_ms[k] / args.steps for k in kernels}
     alg = {"check_pass0": U + U // 8, "inflate_decode": comp_payload, "inflate_resolve": U}
-    names = {"check_pass0": "k_check<0, 1>", "inflate_decode": "k_inflate_decode", "inflate_resolve": "k_inflate_resolve"}
+    names = {"check_pass0": "k_check<0, 1>", "inflate_decode": "k_inflate_decode",
+             "inflate_resolve": "k_inflate_resolve"}
     if args.workload == "load-reads":
         del alg["check_pass0"]
     dom = max(alg, key=lambda k: avg[k])
     achieved = alg[dom] / (avg[dom] * 1e-3) / 1e9 if avg[dom] > 0 else 0.0
     traffic = measured_traffic(names[dom], args) if (args.read_len == 150 and W == 1) else None
 
+    # --- pinned host → results (SURVEY §8(d) "with H2D"): the same step with the shard's compressed bytes in
+    # pinned host memory, streamed in `e2e_windows` windows through two contexts (window w+1's copy overlaps
+    # window w's kernels; window 0's copy is not overlapped).
+    e2e = None
+    if args.e2e_windows > 0 and W == 1 and args.workload == "full-check":
+        if shard is not None:
+            shard.close()
+            shard = None
+        torch.cuda.empty_cache()
+        lo0, hi0 = plan.lo, min(s.size, plan.owned_hi + (64 << 20))
+        host = torch.empty(hi0 - lo0, dtype=torch.uint8, pin_memory=True)
+        hv = host.numpy()
+        s.slice(lo0, hi0, hv)
+
+        def stage_pinned(lo, hi, j):
+            return hv[lo - lo0:hi - lo0] if lo >= lo0 and hi <= hi0 else s.slice(lo, hi)
+
+        epipe = WindowPipe(wplans_of(args.e2e_windows), stage_pinned, split_size, s.contig_lengths, local,
+                           run_window)
+        merge(epipe.step())  # warm-up (allocations)
+        sync()
+        t1 = time.perf_counter()
+        for _ in range(args.e2e_steps):
+            eres, _ = merge(epipe.step())
+        sync()
+        e_el = max_over_ranks(time.perf_counter() - t1)
+        e_ok = sdist.unpack_counts(eres.counts)["n_success"] == int(eres.n_records.sum())
+        epipe.close()
+        e2e = {"value": round(s.size * args.e2e_steps / e_el / 1e9, 3), "unit": "GB/s",
+               "ms_per_step": round(e_el / args.e2e_steps * 1e3, 3), "windows": args.e2e_windows,
+               "steps": args.e2e_steps, "parity_ok": bool(e_ok),
+               "how": "compressed bytes in pinned host memory; each step: sbam_load (H2D) of window 0, then "
+                      "window w+1's H2D on a second context overlapping window w's kernels"}
+        del host
+
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline and args.workload == "full-check" and args.read_len == 150:
             try:
-                cpu = cpu_baseline(args.cpu_sample_mb, args.threads, split_size, args.seed)
+                cpu = cpu_baseline(args.cpu_sample_mb, threads, split_size, args.seed)
+                cpu["host_nproc"] = nproc
             except Exception as e:  # reported, never substituted for the GPU number
                 log(f"cpu baseline failed: {e!r}")
+        try:
+            cpk = copy_peak(dev)
+        except Exception as e:
+            log(f"copy peak failed: {e!r}")
+            cpk = None
         value = s.size * args.steps / elapsed / 1e9
         fc = args.workload == "full-check"
         line = {
@@ -320,19 +449,16 @@ def main():
                          "algorithmic_bytes": alg[dom], "avg_launch_ms": round(avg[dom], 3)},
             "stage_rooflines": {k: {"achieved": round(alg[k] / (avg[k] * 1e-3) / 1e9, 2) if avg[k] > 0 else None,
                                     "algorithmic_bytes": alg[k], "avg_launch_ms": round(avg[k], 3)} for k in alg},
+            "hbm_copy_peak": cpk,
+            "e2e_h2d": e2e,
             "cpu_baseline": cpu,
             "parity": parity,
         }
         print(json.dumps(line), flush=True)
     if shard is not None:
         shard.close()
-    if loader is not None:
-        pending["fut"].result()
-        loader.shutdown()
-        fill_pool.shutdown()
-        for sh in wshards:
-            if sh is not None:
-                sh.close()
+    if pipe is not None:
+        pipe.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -23,9 +23,11 @@ extern "C" {
 /* ---- status codes ---------------------------------------------------------------------------- */
 #define SBAM_OK 0
 #define SBAM_ERR_HEADER_PARSE 1   /* HeaderParseException        bgzf/.../block/HeaderParseException.scala:6-11 */
-#define SBAM_ERR_HEADER_SEARCH 2  /* HeaderSearchFailedException bgzf/.../block/FindBlockStart.scala:31-35   */
+#define SBAM_ERR_HEADER_SEARCH 2  /* HeaderSearchFailedException bgzf/.../block/FindBlockStart.scala:31-35;
+                                     error.position = start, error.actual = positionsAttempted              */
 #define SBAM_ERR_INFLATE 3        /* IOException "Expected N decompressed bytes, found M" Stream.scala:52-54 */
-#define SBAM_ERR_NO_READ_FOUND 4  /* NoReadFoundException        check/.../bam/spark/FindRecordStart.scala:66-71 */
+#define SBAM_ERR_NO_READ_FOUND 4  /* NoReadFoundException        check/.../bam/spark/FindRecordStart.scala:66-71;
+                                     error.position = start, error.expected = maxReadSize                   */
 #define SBAM_ERR_NOT_BAM 5        /* require(magic == "BAM\1")   check/.../bam/header/Header.scala:44-46      */
 #define SBAM_ERR_ARG 6            /* invalid argument / capacity too small                                  */
 #define SBAM_ERR_HIP 7            /* HIP runtime failure (device, allocation, launch)                       */
@@ -92,9 +94,15 @@ void sbam_close(sbam_ctx *ctx);
  * file) and drop every derived stage, keeping the device allocations: the streaming form of sbam_open for
  * inputs larger than HBM, one byte-range window after another (a Spark task re-opening its channel at the
  * next split range).  `data` may be pinned host memory; the copy is on the context's stream, so a second
- * context can load the next window while this one computes. */
+ * context can load the next window while this one computes.  Contig lengths persist only for a later window
+ * of the same file (base_offset > 0 and the same file_size); otherwise sbam_header / sbam_set_contig_lengths
+ * must run again before a check. */
 int sbam_load(sbam_ctx *ctx, const uint8_t *data, int64_t len, int64_t base_offset, int64_t file_size);
 const sbam_error *sbam_last_error(const sbam_ctx *ctx);
+/* The path (Path.toString) that exception messages name, as the reference's HeaderSearchFailedException /
+ * NoReadFoundException format it (HeaderSearchFailedException.scala:7-12, FindRecordStart.scala:66-71);
+ * default "<bytes>". */
+int sbam_set_path(sbam_ctx *ctx, const char *path);
 /* Drop every derived stage (block table, stream, bitmap) but keep the compressed bytes and the device
  * allocations, so the pipeline can be re-run from the resident input without allocating (bench). */
 int sbam_reset(sbam_ctx *ctx);

@@ -61,9 +61,7 @@ struct sbam_ctx {
   int64_t bm_x0 = 0, bm_x1 = 0;
   bool bm_valid = false;
   int32_t bm_R = -1;
-  // inflate scratch: v2 per-lane Huffman tables; token pages of the decode → resolve path
-  uint16_t *d_scratch = nullptr;
-  int nlanes = 0;
+  // inflate scratch: token pages of the decode → resolve path
   uint8_t *d_pool = nullptr;
   size_t pool_cap = 0;  // bytes
   int32_t *d_blkpage = nullptr;
@@ -85,6 +83,7 @@ struct sbam_ctx {
   // timing
   std::map<std::string, std::pair<hipEvent_t, hipEvent_t>> ev;
   sbam_error err{};
+  std::string path = "<bytes>";  // Path.toString in exception messages (sbam_set_path)
 };
 
 namespace {
@@ -164,6 +163,14 @@ int header_parse_error(sbam_ctx *c, int64_t q) {
                      (int)(int8_t)(uint8_t)exps[j]);
     }
   return set_err(c, SBAM_ERR_HEADER_PARSE, "header parse failure at %lld", (long long)(c->base + q));
+}
+
+// NoReadFoundException(path, start, maxReadSize) (FindRecordStart.scala:11-28, 66-71)
+int no_read_found(sbam_ctx *c, int64_t start, int32_t max_read_size) {
+  c->err.position = start;
+  c->err.expected = max_read_size;
+  return set_err(c, SBAM_ERR_NO_READ_FOUND, "Failed to find a valid read-start in %d attempts in %s from %lld",
+                 max_read_size, c->path.c_str(), (long long)start);
 }
 
 int ensure_blocks(sbam_ctx *c) {
@@ -259,7 +266,6 @@ void sbam_close(sbam_ctx *c) {
   dfree(c->d_u);
   dfree(c->d_lens);
   dfree(c->d_bitmap);
-  dfree(c->d_scratch);
   dfree(c->d_pool);
   dfree(c->d_blkpage);
   dfree(c->d_icnt);
@@ -281,6 +287,12 @@ void sbam_close(sbam_ctx *c) {
 
 const sbam_error *sbam_last_error(const sbam_ctx *c) { return c ? &c->err : nullptr; }
 
+int sbam_set_path(sbam_ctx *c, const char *path) {
+  if (!c || !path) return SBAM_ERR_ARG;
+  c->path = path;
+  return SBAM_OK;
+}
+
 int sbam_load(sbam_ctx *c, const uint8_t *data, int64_t len, int64_t base_offset, int64_t file_size) {
   if (!c || (!data && len > 0) || len < 0 || base_offset < 0 || file_size < base_offset + len) return SBAM_ERR_ARG;
   HIPCHK(c, hipSetDevice(c->device));
@@ -289,6 +301,9 @@ int sbam_load(sbam_ctx *c, const uint8_t *data, int64_t len, int64_t base_offset
   HIPCHK(c, hipMemsetAsync(c->d_comp + len, 0, kCompPad, c->stream));
   if (len) HIPCHK(c, hipMemcpyAsync(c->d_comp, data, (size_t)len, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  // another file (or a range from its start): its contig lengths must come from sbam_header /
+  // sbam_set_contig_lengths again; a later window of the same file keeps them
+  if (base_offset == 0 || file_size != c->file_size) c->nref = -1;
   c->D = len;
   c->base = base_offset;
   c->file_size = file_size;
@@ -355,9 +370,11 @@ int sbam_find_block_starts(sbam_ctx *c, const int64_t *starts, int64_t n, int32_
   dfree(d_o);
   for (int64_t i = 0; i < n; i++) {
     if (out[i] < 0) {
+      // HeaderSearchFailedException(path, start, positionsAttempted = MAX_BLOCK_SIZE) (FindBlockStart.scala:16-35)
       c->err.position = starts[i];
-      return set_err(c, SBAM_ERR_HEADER_SEARCH, "Failed to find a BGZF block header in %d bytes from %lld", 65536,
-                     (long long)starts[i]);
+      c->err.actual = 65536;
+      return set_err(c, SBAM_ERR_HEADER_SEARCH, "%s: failed to find BGZF header in %d bytes from %lld",
+                     c->path.c_str(), 65536, (long long)starts[i]);
     }
     out[i] += c->base;
   }
@@ -489,61 +506,43 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
   int32_t *d_status = c->d_status, *d_found = c->d_found;
   const unsigned long long none = ~0ull;
   BlockTable bt{c->d_bstart, c->d_bh, c->d_bc, c->d_bu, c->d_buoff, nb};
-  if (getenv("SBAM_INFLATE_V2")) {  // previous single-kernel path (A/B only)
-    int64_t cap_lanes = 256LL * 512;
-    int lanes = (int)std::min<int64_t>(((nb + 255) / 256) * 256, (cap_lanes / 256) * 256);
-    if (lanes < 256) lanes = 256;
-    if (lanes > c->nlanes) {
-      dfree(c->d_scratch);
-      HIPCHK(c, dalloc(&c->d_scratch, (size_t)lanes * kInflateScratchU16));
-      c->nlanes = lanes;
+  // token pool: ~0.7 B of tokens per output byte on BAM data; a full pool (flagged per block) doubles it
+  // and re-runs, up to the bound of 2 B per output byte (+ one partial page per block)
+  const size_t page_bytes = (size_t)kTokPage, per_page = page_bytes - 16;
+  size_t want = ((size_t)L / per_page + (size_t)nb + 1024) * page_bytes;
+  const size_t bound = (2 * (size_t)L / per_page + 2 * (size_t)nb + 1024) * page_bytes;
+  if (c->pool_cap > want) want = c->pool_cap;
+  HIPCHK(c, ensure(&c->d_blkpage, &c->blkpage_cap, nb));
+  if (!c->d_icnt) HIPCHK(c, dalloc(&c->d_icnt, 4));
+  int dec_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256 * 2);
+  int res_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256 * 4);
+  for (;;) {
+    if (c->pool_cap < want) {
+      dfree(c->d_pool);
+      c->pool_cap = 0;
+      HIPCHK(c, dalloc(&c->d_pool, want));
+      c->pool_cap = want;
     }
-    HIPCHK(c, hipMemcpyAsync(c->d_small + 2, &none, 8, hipMemcpyHostToDevice, c->stream));
-    Timer t(c, "inflate");
-    HIPCHK(c, launch_inflate(c->d_comp, c->D, bt, c->d_u, c->d_scratch, lanes, d_status, d_found,
-                             reinterpret_cast<unsigned int *>(c->d_small + 3),
-                             reinterpret_cast<unsigned long long *>(c->d_small + 2), c->stream));
-  } else {
-    // token pool: ~0.7 B of tokens per output byte on BAM data; a full pool (flagged per block) doubles it
-    // and re-runs, up to the bound of 2 B per output byte (+ one partial page per block)
-    const size_t page_bytes = (size_t)kTokPage, per_page = page_bytes - 16;
-    size_t want = ((size_t)L / per_page + (size_t)nb + 1024) * page_bytes;
-    const size_t bound = (2 * (size_t)L / per_page + 2 * (size_t)nb + 1024) * page_bytes;
-    if (c->pool_cap > want) want = c->pool_cap;
-    HIPCHK(c, ensure(&c->d_blkpage, &c->blkpage_cap, nb));
-    if (!c->d_icnt) HIPCHK(c, dalloc(&c->d_icnt, 4));
-    int dec_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256 * 2);
-    int res_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256 * 4);
-    if (const char *e = getenv("SBAM_DEC_WGS")) dec_wgs = std::max(1, atoi(e));  // A/B sweeps only
-    if (const char *e = getenv("SBAM_RES_WGS")) res_wgs = std::max(1, atoi(e));
-    for (;;) {
-      if (c->pool_cap < want) {
-        dfree(c->d_pool);
-        c->pool_cap = 0;
-        HIPCHK(c, dalloc(&c->d_pool, want));
-        c->pool_cap = want;
-      }
-      const uint32_t npages = (uint32_t)std::min<size_t>(c->pool_cap / page_bytes, 0xffffffffu);
+    const uint32_t npages = (uint32_t)std::min<size_t>(c->pool_cap / page_bytes, 0xffffffffu);
+    {
+      Timer t(c, "inflate");
       {
-        Timer t(c, "inflate");
-        {
-          Timer t1(c, "inflate_decode");
-          HIPCHK(c, launch_inflate_decode(c->d_comp, c->D, bt, c->d_pool, npages, c->d_blkpage, d_status, d_found,
-                                          c->d_icnt, dec_wgs, c->stream));
-        }
-        Timer t2(c, "inflate_resolve");
-        HIPCHK(c, launch_inflate_resolve(bt, c->d_u, c->d_pool, c->d_blkpage, d_found, c->d_icnt, res_wgs,
-                                         c->stream));
+        Timer t1(c, "inflate_decode");
+        HIPCHK(c, launch_inflate_decode(c->d_comp, c->D, bt, c->d_pool, npages, c->d_blkpage, d_status, d_found,
+                                        c->d_icnt, dec_wgs, c->stream));
       }
-      unsigned int used = 0;
-      HIPCHK(c, hipMemcpyAsync(&used, c->d_icnt + 1, 4, hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      if (used <= npages || c->pool_cap >= bound) break;
-      want = std::min(bound, 2 * c->pool_cap);
+      Timer t2(c, "inflate_resolve");
+      HIPCHK(c, launch_inflate_resolve(bt, c->d_u, c->d_pool, c->d_blkpage, d_found, c->d_icnt, res_wgs,
+                                       c->stream));
     }
-    HIPCHK(c, hipMemcpyAsync(c->d_small + 2, &none, 8, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, launch_first_error(d_status, nb, reinterpret_cast<unsigned long long *>(c->d_small + 2), c->stream));
+    unsigned int used = 0;
+    HIPCHK(c, hipMemcpyAsync(&used, c->d_icnt + 1, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (used <= npages || c->pool_cap >= bound) break;
+    want = std::min(bound, 2 * c->pool_cap);
   }
+  HIPCHK(c, hipMemcpyAsync(c->d_small + 2, &none, 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, launch_first_error(d_status, nb, reinterpret_cast<unsigned long long *>(c->d_small + 2), c->stream));
   unsigned long long ferr = 0;
   HIPCHK(c, hipMemcpyAsync(&ferr, c->d_small + 2, 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -879,9 +878,7 @@ static int split_starts(sbam_ctx *c, const sbam_split_args *a, int64_t first, in
   for (int64_t i = 0; i < count; i++) {
     const int64_t b = block_at(c, bs[i] - c->base);
     if (b < 0) {  // FindRecordStart on the EOF marker: empty stream → None → NoReadFoundException
-      c->err.position = st[first + i];
-      return set_err(c, SBAM_ERR_NO_READ_FOUND, "Failed to find a valid read-start in %d attempts in %s from %lld",
-                     a->max_read_size, "path", (long long)bs[i]);
+      return no_read_found(c, bs[i], a->max_read_size);
     }
     x0[i] = c->h_buoff[b];
     xe[i] = x_end_of(c, en[first + i] - c->base);
@@ -891,9 +888,7 @@ static int split_starts(sbam_ctx *c, const sbam_split_args *a, int64_t first, in
   for (int64_t i = 0; i < count; i++) {
     if (xs[i] == -2) return set_err(c, SBAM_ERR_HALO, "record search left the shard");
     if (xs[i] < 0) {
-      c->err.position = bs[i];
-      return set_err(c, SBAM_ERR_NO_READ_FOUND, "Failed to find a valid read-start in %d attempts in %s from %lld",
-                     a->max_read_size, "path", (long long)bs[i]);
+      return no_read_found(c, bs[i], a->max_read_size);
     }
   }
   return SBAM_OK;

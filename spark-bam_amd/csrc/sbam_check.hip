@@ -19,15 +19,9 @@
 
 #include "sbam_internal.h"
 
-#ifndef SBAM_ABLATE
-#define SBAM_ABLATE 0
-#endif
-#ifndef SBAM_CHECK_WGS  // k_check workgroups per CU the register budget is sized for (launch bounds)
+// k_check workgroups per CU the register budget is sized for (launch bounds): boundary tiles / interior tiles
 #define SBAM_CHECK_WGS 4
-#endif
-#ifndef SBAM_CHECK_WGS_INT  // the same for the interior-tiles-only instantiation
 #define SBAM_CHECK_WGS_INT 5
-#endif
 
 namespace sbam {
 
@@ -842,9 +836,6 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
       v |= shfl_xor64(v, 8);
       if ((lane & 15) == 0 && (INTERIOR || xg < x1)) bitmap[(xg - x0a) >> 6] = v;  // word holds >= 1 position < x1
       if (!COUNTS) continue;
-#if SBAM_ABLATE == 3  // timing experiment only: no counting
-      continue;
-#endif
       uint32_t Fo[4];
       if constexpr (INTERIOR && !BYKEY) {
         uint32_t oh[4];

@@ -51,10 +51,7 @@ constexpr int kEpoch = 4;          // iterations between input-window slides and
 // A lane that reaches a block header parks; parked lanes build their tables together once kParkMin of the
 // wave's 64 lanes wait (or none is left decoding): a table build is a serial loop of a few thousand
 // instructions per lane, and builds started one lane at a time would cost the whole wave that much each.
-#ifndef SBAM_PARK_MIN
-#define SBAM_PARK_MIN 16
-#endif
-constexpr int kParkMin = SBAM_PARK_MIN;
+constexpr int kParkMin = 16;
 
 constexpr uint8_t kClOrder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
@@ -255,20 +252,6 @@ SB_DEV bool tok_put(TokOut &to, uint32_t t, uint8_t *pool, unsigned int *pool_ne
 
 enum : int { S_NEXT = 0, S_HDR = 1, S_HUFF = 2, S_STORED = 3, S_DONE = 4, S_EXIT = 5, S_PARK = 6 };
 
-// Diagnostic build only (-DSBAM_DEC_STATS): per-wave cycle attribution of the decode loop, summed over waves.
-#ifdef SBAM_DEC_STATS
-__device__ unsigned long long g_dec_stats[16];
-#define DSTAT_MARK(slot)                                  \
-  do {                                                    \
-    const uint64_t t_ = __builtin_amdgcn_s_memtime();     \
-    ds_[slot] += t_ - dt_;                                \
-    dt_ = t_;                                             \
-  } while (0)
-#define DSTAT_ADD(slot, v) ds_[slot] += (v)
-#else
-#define DSTAT_MARK(slot) do {} while (0)
-#define DSTAT_ADD(slot, v) do {} while (0)
-#endif
 
 // Bit reader.  bb holds bc valid bits (LSB first); rp = block-relative index of the next payload dword to enter
 // bb; left = payload bits not yet consumed (negative ⇒ the symbol needed bits past the payload: zlib returns
@@ -321,11 +304,6 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
   TokOut to{0, 0, 0, 0, 0, 0, 0, 0, 0, false, 0};
   Canon lc, dc;
   int32_t o = 0, us = 0, err = INF_OK, sleft = 0, fin = 0;
-#ifdef SBAM_DEC_STATS
-  uint64_t ds_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  uint64_t dt_ = __builtin_amdgcn_s_memtime();
-  const uint64_t dt0_ = dt_;
-#endif
   auto refill = [&]() {  // the symbol loop's refill: next dword from the register window
     if (br.bc <= 32) {
       br.bb |= (uint64_t)br.nx << br.bc;
@@ -386,14 +364,7 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
       const uint64_t pk = __ballot(state == S_PARK);
       const uint64_t dc = __ballot(state == S_HUFF || state == S_STORED);
       if (pk && (__popcll(pk) >= kParkMin || dc == 0) && state == S_PARK) state = S_HDR;
-      DSTAT_ADD(5, 1);
-      DSTAT_ADD(7, __popcll(dc));
-      DSTAT_ADD(8, __popcll(pk));
     }
-    DSTAT_MARK(0);
-#ifdef SBAM_DEC_STATS
-    const bool any_hdr_ = __ballot(state == S_HDR) != 0;
-#endif
 
     // --- epoch (wave-uniform): slide the input window, store the pending token chunk, issue the next loads
     if ((it & (kEpoch - 1)) == 0) {
@@ -419,8 +390,6 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
         to.pend = false;
       }
     }
-
-    DSTAT_MARK(1);
     if (state == S_HDR) {
       // --- block header (RFC 1951 §3.2.3); every read checks that the payload holds the bits (else SHORT)
       br.refill_hbm(src);
@@ -728,10 +697,6 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
         }
       }
     }
-#ifdef SBAM_DEC_STATS
-    DSTAT_MARK(any_hdr_ ? 2 : 3);
-    DSTAT_ADD(6, any_hdr_ ? 1 : 0);
-#endif
     if (state == S_DONE) {
       if (err != INF_OVERFLOW) {  // final (padded) chunk and any pending one leave now
         bool ok = true;
@@ -746,13 +711,7 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
       found[blk] = err == INF_OVERFLOW ? 0 : o;  // an overflowed block has no complete token stream
       state = S_NEXT;
     }
-    DSTAT_MARK(4);
   }
-#ifdef SBAM_DEC_STATS
-  ds_[9] = __builtin_amdgcn_s_memtime() - dt0_;
-  if (__lane_id() == 0)
-    for (int i = 0; i < 10; i++) atomicAdd(&g_dec_stats[i], (unsigned long long)ds_[i]);
-#endif
 }
 
 // ---- resolve kernel -------------------------------------------------------------------------------------------
@@ -762,23 +721,23 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
 // (the line is written whole while it is still in L2); a far copy is one unaligned 16-B load.
 constexpr int kResThreads = 256;
 constexpr int kResRing = 136;  // per-lane ring stride (128 B used): 34 dwords, 8-B aligned
-// Copies with (effective) distance <= kNear read the ring, longer ones HBM.  The flushed mark trails the output
-// by < 64 B when a copy starts, so a source 80 B back is stored; the ring still holds 105 B behind the output.
+// Copies with (effective) distance <= kNear read the ring, longer ones HBM.  Ring invariants (128-B ring):
+//  * the flushed mark trails the output by <= 63 B when a step starts, and a copy step writes 16 bytes at the
+//    output, so a far copy's 16-B source [a - eff, a - eff + 16) lies below the flushed mark when eff >= 63 + 16
+//    = 79, i.e. for every eff > kNear;
+//  * a step advances the output by at most 16 + kResLits - 1 (a copy, then the literals after it) and writes
+//    ring bytes up to 3 past that (the dword-aligned 16-B scratch write), so the bytes it touches stay clear of
+//    the kNear-byte window a near copy reads behind the output and of the unflushed group.
 constexpr int kNear = 80;
-// Literals a step may take (the first token plus up to kResLits - 1 more literals already in the current chunk).
-#ifndef SBAM_RES_LITS
-#define SBAM_RES_LITS 4
-#endif
-constexpr int kResLits = SBAM_RES_LITS;
-static_assert(kResLits >= 1 && kResLits <= 8, "a step writes at most 16 ring bytes");
+constexpr int kResLits = 4;  // literals a step may take (the first token plus up to kResLits - 1 more)
+static_assert(63 + 16 <= kNear + 1, "far copies read only flushed output");
+static_assert(kNear + 16 + kResLits + 3 <= 128, "a step's ring writes never reach the near window");
 
 // Tokens are read a group of kTokGroupChunks 16-B chunks at a time (aligned; a page's first group starts with
 // the next-page link).
-#ifndef SBAM_TOK_GROUP
-#define SBAM_TOK_GROUP 128
-#endif
-constexpr int kTG = SBAM_TOK_GROUP / 16;  // chunks per token group
-static_assert(kTG >= 2 && (kTokPage % SBAM_TOK_GROUP) == 0, "token groups tile a page");
+constexpr int kTokGroup = 128;
+constexpr int kTG = kTokGroup / 16;  // chunks per token group
+static_assert(kTG >= 2 && (kTokPage % kTokGroup) == 0, "token groups tile a page");
 
 struct TokIn {
   uint32_t t0, t1, t2, t3;      // current chunk (t0 low half = next token)
@@ -1001,16 +960,6 @@ hipError_t launch_first_error(const int32_t *status, int64_t n, unsigned long lo
   return hipGetLastError();
 }
 
-#ifdef SBAM_DEC_STATS
-extern "C" int sbam_debug_decode_stats(unsigned long long *out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dec_stats), sizeof(g_dec_stats)) != hipSuccess) return -1;
-  if (reset) {
-    static const unsigned long long z[16] = {0};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dec_stats), z, sizeof(z)) != hipSuccess) return -1;
-  }
-  return 0;
-}
-#endif
 
 hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *pool, uint32_t npages,
                                  int32_t *blk_page, int32_t *status, int32_t *found, unsigned int *counters,

@@ -53,7 +53,6 @@ struct RecordColumnsDev {
 };
 
 constexpr int kScanChunk = 1 << 20;  // bytes per workgroup in the BGZF candidate scan
-constexpr int kInflateScratchU16 = 2048;  // per-lane Huffman table scratch (u16 entries)
 constexpr int kStreamPad = 16384;  // zero pad behind the uncompressed stream (>= checker LDS window)
 constexpr int kCompPad = 256;  // zero pad behind the compressed bytes (bit-reader / input-ring lookahead)
 constexpr uint64_t kTokPage = 4096;  // inflate token page: 16-B header (next page) + 255 chunks of 8 u16 tokens
@@ -70,9 +69,6 @@ hipError_t launch_find_block_starts(const uint8_t *d, int64_t D, const Candidate
                                     hipStream_t s);
 hipError_t launch_gather_blocks(const Candidate *cands, int64_t first, int64_t n, int64_t *start, int32_t *hsize,
                                 int32_t *csize, int32_t *usize, hipStream_t s);
-hipError_t launch_inflate(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *out, uint16_t *scratch, int nlanes,
-                          int32_t *status, int32_t *found, unsigned int *next_block, unsigned long long *first_err,
-                          hipStream_t s);
 // Two-kernel inflate (sbam_inflate.hip): entropy decode into token pages, then LZ77 resolve into `out`.
 // counters: 3 × u32 device scratch (decode work, pool pages used, resolve work), reset by the decode launch.
 hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *pool, uint32_t npages,

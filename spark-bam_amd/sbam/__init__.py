@@ -110,7 +110,7 @@ RECORD_COLUMNS = {"offset": np.int64, "block_pos": np.int64, "block_off": np.int
 
 
 EXPORTS = [  # every symbol include/sbam.h declares
-    "sbam_open", "sbam_close", "sbam_load", "sbam_last_error", "sbam_reset", "sbam_version", "sbam_find_block_starts", "sbam_scan_blocks",
+    "sbam_open", "sbam_close", "sbam_load", "sbam_last_error", "sbam_set_path", "sbam_reset", "sbam_version", "sbam_find_block_starts", "sbam_scan_blocks",
     "sbam_get_blocks", "sbam_inflate", "sbam_read_uncompressed", "sbam_pos_to_offset", "sbam_offset_to_pos",
     "sbam_header", "sbam_set_contig_lengths", "sbam_check_eager", "sbam_check_full_words", "sbam_check_full_counts",
     "sbam_find_record_start", "sbam_file_splits", "sbam_split_records", "sbam_compute_splits",
@@ -119,6 +119,19 @@ EXPORTS = [  # every symbol include/sbam.h declares
 ]
 
 _lib = None
+
+
+def source_digest() -> str:
+    """Digest of the kernel and C-ABI sources libsbam.so is built from: ties committed profiles (PMC traffic) to
+    the kernel build they were measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(_HERE, "..", "csrc")
+    for name in sorted(os.listdir(csrc)):
+        if name.endswith((".hip", ".cpp", ".h")):
+            with open(os.path.join(csrc, name), "rb") as fh:
+                h.update(name.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
 
 
 def load_library(path: str = LIB_PATH):
@@ -134,6 +147,7 @@ def load_library(path: str = LIB_PATH):
         "sbam_open": (ctypes.c_int, [ctypes.c_int, vp, i64, i64, i64, P(vp)]),
         "sbam_close": (None, [vp]),
         "sbam_last_error": (P(_Error), [vp]),
+        "sbam_set_path": (ctypes.c_int, [vp, ctypes.c_char_p]),
         "sbam_reset": (ctypes.c_int, [vp]),
         "sbam_version": (ctypes.c_char_p, []),
         "sbam_find_block_starts": (ctypes.c_int, [vp, vp, i64, i32, vp]),
@@ -254,6 +268,7 @@ class BamFile:
         rc = self.L.sbam_open(device, _ptr(self._buf), self._buf.size, base_offset, self.file_size,
                               ctypes.byref(self.ctx))
         self._check(rc)
+        self._check(self.L.sbam_set_path(self.ctx, str(path).encode()))
         self.n_blocks = self._scan()
         self.uncompressed_size = None
         self.n_ref = None

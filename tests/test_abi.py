@@ -78,3 +78,115 @@ def test_load_window_gpu():
             f.load(a)
             f.run()
             assert f.blocks()[0].size == 25 and int(f.check_eager(0, f.uncompressed_size).sum()) == 4917
+
+
+def test_struct_layout_matches_compiled_c(tmp_path):
+    """sizeof/offsetof of the ABI structs as a C compiler lays out include/sbam.h, against the ctypes mirror and
+    the offsets INTEGRATION.md's Panama binding reads (message @32, sizeof(sbam_error) = 544)."""
+    import subprocess
+    import sbam
+    probe = tmp_path / "probe.c"
+    fields = {
+        "sbam_error": ["code", "idx", "actual", "expected", "position", "message"],
+        "sbam_pos": ["block_pos", "offset", "reserved"],
+        "sbam_split": ["start", "end"],
+        "sbam_counts": ["totals", "counts", "positions", "reads_before_error", "pair_hist", "n_positions",
+                        "n_success", "n_too_few_fixed", "n_halo"],
+        "sbam_split_args": ["split_size", "bgzf_blocks_to_check", "reads_to_check", "max_read_size",
+                            "use_success_bitmap"],
+        "sbam_record_columns": list(sbam.RECORD_COLUMNS),
+    }
+    lines = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{ROOT}/include/sbam.h"', "int main(void) {"]
+    for t, fs in fields.items():
+        lines.append(f'  printf("{t} sizeof %zu\\n", sizeof({t}));')
+        for f in fs:
+            lines.append(f'  printf("{t} {f} %zu\\n", offsetof({t}, {f}));')
+    lines += ["  return 0;", "}"]
+    probe.write_text("\n".join(lines))
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-o", str(exe), str(probe)], check=True)
+    c = {}
+    for ln in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.splitlines():
+        t, f, v = ln.split()
+        c[(t, f)] = int(v)
+    mirror = {"sbam_error": sbam._Error, "sbam_pos": sbam._Pos, "sbam_split": sbam._Split,
+              "sbam_counts": sbam._Counts, "sbam_split_args": sbam._SplitArgs,
+              "sbam_record_columns": sbam._RecordColumns}
+    for t, cls in mirror.items():
+        assert c[(t, "sizeof")] == ctypes.sizeof(cls), t
+        for f in fields[t]:
+            assert c[(t, f)] == getattr(cls, f).offset, (t, f)
+    assert c[("sbam_error", "message")] == 32 and c[("sbam_error", "sizeof")] == 544
+    assert c[("sbam_error", "position")] == 24 and c[("sbam_error", "actual")] == 8
+    assert c[("sbam_error", "expected")] == 16
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    assert "err.getString(32)" in text and "byteSize() == 544" in text
+
+
+@pytest.mark.gpu
+def test_error_messages_name_the_path():
+    """HeaderSearchFailedException / NoReadFoundException messages as the reference formats them
+    (HeaderSearchFailedException.scala:7-12, FindRecordStart.scala:66-71) with the path set by sbam_set_path, and
+    the structured fields a JVM shim rebuilds them from."""
+    import numpy as np
+    import sbam
+    from conftest import fixture_bytes
+    # a shard whose first 65536 bytes hold no BGZF header: FindBlockStart(1000) fails
+    with pytest.raises(sbam.HeaderSearchFailedException) as ei:
+        sbam.BamFile(np.zeros(140000, np.uint8), base_offset=1000, file_size=141000, path="holes.bam")
+    assert str(ei.value) == "holes.bam: failed to find BGZF header in 65536 bytes from 1000"
+    # a Hadoop split starting past the last data block: FindBlockStart returns the EOF marker, the stream from
+    # there is empty, FindRecordStart throws
+    data = fixture_bytes("2.bam")
+    L = len(data)
+    with sbam.BamFile(data, path="test_bams/2.bam") as f:
+        st = f.blocks()[0]
+        last, eof = int(st[-1]), L - 28
+        S = next(S for S in range(max(1, (eof - last) // 3), eof - last + 1)
+                 if any(last < a <= eof for a, _ in sbam.hadoop_splits(L, S)))
+        with pytest.raises(sbam.NoReadFoundException) as ei:
+            f.compute_splits(S)
+        e = f.L.sbam_last_error(f.ctx).contents
+        assert e.code == sbam.ERR_NO_READ_FOUND and e.position == eof and e.expected == sbam.MAX_READ_SIZE
+        assert str(ei.value) == f"Failed to find a valid read-start in {sbam.MAX_READ_SIZE} attempts in test_bams/2.bam from {eof}"
+
+
+@pytest.mark.gpu
+def test_concurrent_handles_match_serial():
+    """§8(b) reentrancy: 4 threads × 4 handles (one per thread at a time, all on one GPU) give the serial results
+    — no global mutable state, each handle its own stream and allocations."""
+    import threading
+    import numpy as np
+    import sbam
+    from conftest import fixture_bytes
+    names = ["1.bam", "2.bam", "5k.bam", "1.2203053-2211029.bam"]
+    want = {}
+    for nm in names:
+        with sbam.BamFile(fixture_bytes(nm), path=nm) as f:
+            c = f.check_full_counts()
+            want[nm] = (f.uncompressed_size, c.totals.copy(), c.n_success,
+                        [str(s) for s in f.compute_splits(100000)], f.check_eager().copy())
+    errors = []
+
+    def worker(k):
+        try:
+            for j in range(4):
+                nm = names[(k + j) % 4]
+                with sbam.BamFile(fixture_bytes(nm), path=nm) as f:
+                    c = f.check_full_counts()
+                    got = (f.uncompressed_size, c.totals, c.n_success, [str(s) for s in f.compute_splits(100000)],
+                           f.check_eager())
+                    w = want[nm]
+                    ok = got[0] == w[0] and np.array_equal(got[1], w[1]) and got[2] == w[2] and got[3] == w[3] \
+                        and np.array_equal(got[4], w[4])
+                    if not ok:
+                        errors.append((k, nm))
+        except Exception as e:  # noqa: BLE001
+            errors.append((k, repr(e)))
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors

@@ -46,7 +46,11 @@ def main():
     a = ap.parse_args()
     fetch, nf = per_dispatch(a.fetch_dir, "FETCH_SIZE")
     write, nw = per_dispatch(a.write_dir, "WRITE_SIZE")
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "spark-bam_amd"))
+    import sbam
     out = {"workload": {"size_gb": a.size_gb, "seed": a.seed, "tile_mb": a.tile_mb},
+           "source_digest": sbam.source_digest(),
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes of tools/bench_kernels.py; "
                      "median dispatch; FETCH x2 (gfx950 64-B tally of 128-B requests), WRITE as reported",
            "kernels": {}}
