@@ -127,6 +127,10 @@ int sbam_get_blocks(sbam_ctx *ctx, int64_t *start, int32_t *csize, int32_t *usiz
  * (Stream.scala:31-71 with Inflater(nowrap=true)); *uncompressed_size receives its length. */
 int sbam_inflate(sbam_ctx *ctx, int64_t *uncompressed_size);
 
+/* Blocks the last sbam_inflate handed from the wave-parallel decoder to the exact per-lane one (stored or
+ * invalid blocks, incomplete codes, streams that end before ISIZE or run past it); for parity tests and profiles. */
+int sbam_inflate_fallbacks(sbam_ctx *ctx, int64_t *n);
+
 /* Copy uncompressed bytes [off, off+len) of the stream to the host. */
 int sbam_read_uncompressed(sbam_ctx *ctx, int64_t off, int64_t len, uint8_t *out);
 

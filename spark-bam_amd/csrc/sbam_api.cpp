@@ -62,11 +62,12 @@ struct sbam_ctx {
   bool bm_valid = false;
   int32_t bm_R = -1;
   // inflate scratch: token pages of the decode → resolve path
-  uint8_t *d_pool = nullptr;
-  size_t pool_cap = 0;  // bytes
-  int32_t *d_blkpage = nullptr;
-  size_t blkpage_cap = 0;
-  unsigned int *d_icnt = nullptr;  // decode work, pool pages used, resolve work
+  uint8_t *d_pool = nullptr;  // token regions (inflate_token_bytes)
+  size_t pool_cap = 0;
+  int32_t *d_slow = nullptr;  // blocks the wave decoder hands to the exact per-lane decoder
+  size_t slow_cap = 0;
+  unsigned int *d_icnt = nullptr;  // slow-path blocks, slow-path work, resolve work
+  int64_t inflate_slow = -1;       // blocks the last sbam_inflate decoded on the exact per-lane path
   // split chains: per-split first record / chain end / count / record base (grow-only)
   int64_t *d_sx = nullptr, *d_se = nullptr, *d_sn = nullptr, *d_sb = nullptr;
   size_t sx_cap = 0, se_cap = 0, sn_cap = 0, sb_cap = 0;
@@ -267,7 +268,7 @@ void sbam_close(sbam_ctx *c) {
   dfree(c->d_lens);
   dfree(c->d_bitmap);
   dfree(c->d_pool);
-  dfree(c->d_blkpage);
+  dfree(c->d_slow);
   dfree(c->d_icnt);
   dfree(c->d_small);
   dfree(c->d_counts);
@@ -506,46 +507,29 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
   int32_t *d_status = c->d_status, *d_found = c->d_found;
   const unsigned long long none = ~0ull;
   BlockTable bt{c->d_bstart, c->d_bh, c->d_bc, c->d_bu, c->d_buoff, nb};
-  // token pool: ~0.7 B of tokens per output byte on BAM data; a full pool (flagged per block) doubles it
-  // and re-runs, up to the bound of 2 B per output byte (+ one partial page per block)
-  const size_t page_bytes = (size_t)kTokPage, per_page = page_bytes - 16;
-  size_t want = ((size_t)L / per_page + (size_t)nb + 1024) * page_bytes;
-  const size_t bound = (2 * (size_t)L / per_page + 2 * (size_t)nb + 1024) * page_bytes;
-  if (c->pool_cap > want) want = c->pool_cap;
-  HIPCHK(c, ensure(&c->d_blkpage, &c->blkpage_cap, nb));
+  // token regions: every block's tokens at a fixed offset (at most 2 B per output byte), so no pool overflow
+  HIPCHK(c, ensure(&c->d_pool, &c->pool_cap, inflate_token_bytes(L, nb)));
+  HIPCHK(c, ensure(&c->d_slow, &c->slow_cap, nb));
   if (!c->d_icnt) HIPCHK(c, dalloc(&c->d_icnt, 4));
-  int dec_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256 * 2);
-  int res_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256 * 4);
-  for (;;) {
-    if (c->pool_cap < want) {
-      dfree(c->d_pool);
-      c->pool_cap = 0;
-      HIPCHK(c, dalloc(&c->d_pool, want));
-      c->pool_cap = want;
-    }
-    const uint32_t npages = (uint32_t)std::min<size_t>(c->pool_cap / page_bytes, 0xffffffffu);
+  const int res_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256 * 4);
+  {
+    Timer t(c, "inflate");
     {
-      Timer t(c, "inflate");
-      {
-        Timer t1(c, "inflate_decode");
-        HIPCHK(c, launch_inflate_decode(c->d_comp, c->D, bt, c->d_pool, npages, c->d_blkpage, d_status, d_found,
-                                        c->d_icnt, dec_wgs, c->stream));
-      }
-      Timer t2(c, "inflate_resolve");
-      HIPCHK(c, launch_inflate_resolve(bt, c->d_u, c->d_pool, c->d_blkpage, d_found, c->d_icnt, res_wgs,
-                                       c->stream));
+      Timer t1(c, "inflate_decode");
+      HIPCHK(c, launch_inflate_decode(c->d_comp, c->D, bt, c->d_pool, d_status, d_found, c->d_slow, c->d_icnt,
+                                      c->stream));
     }
-    unsigned int used = 0;
-    HIPCHK(c, hipMemcpyAsync(&used, c->d_icnt + 1, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (used <= npages || c->pool_cap >= bound) break;
-    want = std::min(bound, 2 * c->pool_cap);
+    Timer t2(c, "inflate_resolve");
+    HIPCHK(c, launch_inflate_resolve(bt, c->d_u, c->d_pool, d_found, c->d_icnt, res_wgs, c->stream));
   }
   HIPCHK(c, hipMemcpyAsync(c->d_small + 2, &none, 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, launch_first_error(d_status, nb, reinterpret_cast<unsigned long long *>(c->d_small + 2), c->stream));
   unsigned long long ferr = 0;
+  unsigned int nslow = 0;
   HIPCHK(c, hipMemcpyAsync(&ferr, c->d_small + 2, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(&nslow, c->d_icnt, 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->inflate_slow = nslow;
   if (ferr != ~0ull) {
     int32_t found = 0;
     HIPCHK(c, hipMemcpy(&found, d_found + ferr, 4, hipMemcpyDeviceToHost));
@@ -557,6 +541,13 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
   c->L = L;
   c->bm_valid = false;
   if (usz) *usz = L;
+  return SBAM_OK;
+}
+
+int sbam_inflate_fallbacks(sbam_ctx *c, int64_t *n) {
+  if (!c || !n) return SBAM_ERR_ARG;
+  if (c->L < 0 && c->inflate_slow < 0) return set_err(c, SBAM_ERR_STATE, "sbam_inflate has not run");
+  *n = c->inflate_slow;
   return SBAM_OK;
 }
 

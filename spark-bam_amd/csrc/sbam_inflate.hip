@@ -29,11 +29,16 @@ namespace sbam {
 
 enum : int32_t { INF_OK = 0, INF_SHORT = 1, INF_DATA = 2, INF_OVERFLOW = 3 };
 
-// ---- token pages ------------------------------------------------------------------------------------------
-// A page is kTokPage bytes: chunk 0 holds the index of the block's next page (dword 0), chunks 1..255 hold
-// tokens (8 × u16 per 16-B chunk).  Token t < 256: literal byte t.  256 <= t < 512: match of length t - 253,
-// followed by the token (distance - 1).  0xffff: padding.
+// ---- tokens ---------------------------------------------------------------------------------------------------
+// Token t < 256: literal byte t.  256 <= t < 512: match of length t - 253, followed by the token (distance - 1).
+// 0xffff: padding (the slow decoder keeps a length and its distance in one 16-B chunk).
 constexpr uint32_t kTokPad = 0xffffu;
+
+// Block b's tokens are u16s in the 16-B aligned region tok_region(uoff[b], b) of the token buffer.  A block yields
+// at most ISIZE tokens plus 8 of padding (slow decoder), and regions 2 uoff + 32 b apart never overlap.
+SB_DEV uint64_t tok_region(int64_t uoff, int64_t b) {
+  return (((uint64_t)uoff * 2 + 15) & ~15ull) + 32ull * (uint64_t)b;
+}
 
 // ---- decode kernel --------------------------------------------------------------------------------------------
 // Per-lane tables live in LDS, interleaved across the workgroup's lanes at dword granularity (byte b of lane L at
@@ -217,30 +222,23 @@ struct TokOut {
   uint64_t cur;  // byte offset of the next chunk in the pool
 };
 
-// Store one chunk; open a new page when this one is full.  Returns false on pool overflow.
-SB_DEV bool tok_store(TokOut &to, uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint8_t *pool,
-                      unsigned int *pool_next, uint32_t npages) {
+// Store one chunk into the block's token region (tok_region: room for every token the block can produce).
+SB_DEV bool tok_store(TokOut &to, uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint8_t *pool) {
   *reinterpret_cast<uint4 *>(pool + to.cur) = make_uint4(a, b, c, d);
   to.cur += 16;
-  if ((to.cur & (kTokPage - 1)) == 0) {
-    const uint32_t pg = atomicAdd(pool_next, 1u);
-    if (pg >= npages) return false;
-    *reinterpret_cast<uint32_t *>(pool + to.cur - kTokPage) = pg;  // link from the page just filled
-    to.cur = (uint64_t)pg * kTokPage + 16;
-  }
   return true;
 }
 
 // Append one token; a completed chunk becomes pending (an older pending chunk is stored first: only at a
 // block's end or when more than 8 tokens arrive within one epoch).
-SB_DEV bool tok_put(TokOut &to, uint32_t t, uint8_t *pool, unsigned int *pool_next, uint32_t npages) {
+SB_DEV bool tok_put(TokOut &to, uint32_t t, uint8_t *pool) {
   to.t0 = __builtin_amdgcn_alignbit(to.t1, to.t0, 16);
   to.t1 = __builtin_amdgcn_alignbit(to.t2, to.t1, 16);
   to.t2 = __builtin_amdgcn_alignbit(to.t3, to.t2, 16);
   to.t3 = __builtin_amdgcn_alignbit(t, to.t3, 16);
   if (++to.n < 8) return true;
   bool ok = true;
-  if (to.pend) ok = tok_store(to, to.p0, to.p1, to.p2, to.p3, pool, pool_next, npages);
+  if (to.pend) ok = tok_store(to, to.p0, to.p1, to.p2, to.p3, pool);
   to.p0 = to.t0;
   to.p1 = to.t1;
   to.p2 = to.t2;
@@ -277,13 +275,13 @@ struct Bits {
   }
 };
 
-__global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t *__restrict__ d, int64_t D,
-                                                                   BlockTable bt, uint8_t *__restrict__ pool,
-                                                                   uint32_t npages, unsigned int *pool_next,
-                                                                   int32_t *__restrict__ blk_page,
-                                                                   int32_t *__restrict__ status,
-                                                                   int32_t *__restrict__ found,
-                                                                   unsigned int *next_block) {
+__global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *__restrict__ d, int64_t D,
+                                                                 BlockTable bt, uint8_t *__restrict__ pool,
+                                                                 const int32_t *__restrict__ slow,
+                                                                 const unsigned int *nslow,
+                                                                 int32_t *__restrict__ status,
+                                                                 int32_t *__restrict__ found,
+                                                                 unsigned int *next_block) {
   __shared__ __attribute__((aligned(16))) uint8_t s_dec[kRows * kDecThreads * 4];
   const Slice sl{s_dec + 4 * threadIdx.x};
   const uint32_t *d32 = reinterpret_cast<const uint32_t *>(d);
@@ -315,10 +313,11 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
 
   for (int it = 0;; it++) {
     if (state == S_NEXT) {
-      blk = (int64_t)atomicAdd(next_block, 1u);
-      if (blk >= bt.n) {
+      const uint32_t i = atomicAdd(next_block, 1u);
+      if (i >= *nslow) {
         state = S_EXIT;
       } else {
+        blk = slow[i];
         const int64_t st = bt.start[blk];
         const int32_t hs = bt.hsize[blk], cs = bt.csize[blk];
         us = bt.usize[blk];
@@ -326,20 +325,14 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
         fin = 0;
         err = INF_OK;
         const int32_t dlen = cs - hs - 8;  // Stream.scala: dataLength = compressedSize - headerSize - FOOTER_SIZE
-        blk_page[blk] = -1;
         if (us == 0) {
           state = S_DONE;  // inflate(buf, 0, 0) returns 0
         } else if (us < 0 || us > 65536 || dlen < 0 || st + hs + dlen > D) {
           err = INF_DATA;
           state = S_DONE;
         } else {
-          const uint32_t p = atomicAdd(pool_next, 1u);
-          if (p >= npages) {
-            err = INF_OVERFLOW;
-            state = S_DONE;
-          } else {
-            blk_page[blk] = (int32_t)p;
-            to.cur = (uint64_t)p * kTokPage + 16;
+          {
+            to.cur = tok_region(bt.uoff[blk], blk);
             to.n = 0;
             to.pend = false;
             // word pointer derived from d by arithmetic only (an integer round trip would make it a flat
@@ -383,10 +376,7 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
         }
       }
       if (to.pend && (dec || state == S_PARK || state == S_HDR)) {
-        if (!tok_store(to, to.p0, to.p1, to.p2, to.p3, pool, pool_next, npages)) {
-          err = INF_OVERFLOW;
-          state = S_DONE;
-        }
+        tok_store(to, to.p0, to.p1, to.p2, to.p3, pool);
         to.pend = false;
       }
     }
@@ -595,7 +585,7 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
         int len = 0;
         bool is_len = false;
         if (sym < 256) {
-          if (!tok_put(to, (uint32_t)sym, pool, pool_next, npages)) err = INF_OVERFLOW;
+          if (!tok_put(to, (uint32_t)sym, pool)) err = INF_OVERFLOW;
           o++;
           if (o == us || err != INF_OK) state = S_DONE;
         } else if (sym == 256) {
@@ -629,7 +619,7 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
           if (!is_len) {
             if (v2 && i2 < h2 && br.left >= L2) {
               br.drop(L2);
-              if (!tok_put(to, (uint32_t)b2, pool, pool_next, npages)) err = INF_OVERFLOW;
+              if (!tok_put(to, (uint32_t)b2, pool)) err = INF_OVERFLOW;
               o++;
               if (o == us || err != INF_OK) state = S_DONE;
             }
@@ -656,9 +646,9 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
                   state = S_DONE;
                 } else {
                   bool ok = true;
-                  if (to.n == 7) ok = tok_put(to, kTokPad, pool, pool_next, npages);  // a match never straddles
-                  ok = ok && tok_put(to, (uint32_t)(len + 253), pool, pool_next, npages);
-                  ok = ok && tok_put(to, (uint32_t)(dist - 1), pool, pool_next, npages);
+                  if (to.n == 7) ok = tok_put(to, kTokPad, pool);  // a match never straddles
+                  ok = ok && tok_put(to, (uint32_t)(len + 253), pool);
+                  ok = ok && tok_put(to, (uint32_t)(dist - 1), pool);
                   if (!ok) err = INF_OVERFLOW;
                   o = min(o + len, us);
                   if (o == us || err != INF_OK) state = S_DONE;
@@ -675,7 +665,7 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
       int m = 0;
       for (int i = 0; i < 2; i++) {
         if (i < n && br.left >= 8 && err == INF_OK) {
-          if (!tok_put(to, br.peek(8), pool, pool_next, npages)) err = INF_OVERFLOW;
+          if (!tok_put(to, br.peek(8), pool)) err = INF_OVERFLOW;
           br.drop(8);
           m++;
         }
@@ -701,8 +691,8 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
       if (err != INF_OVERFLOW) {  // final (padded) chunk and any pending one leave now
         bool ok = true;
         if (to.n > 0)
-          while (ok && to.n > 0) ok = tok_put(to, kTokPad, pool, pool_next, npages);
-        if (ok && to.pend) ok = tok_store(to, to.p0, to.p1, to.p2, to.p3, pool, pool_next, npages);
+          while (ok && to.n > 0) ok = tok_put(to, kTokPad, pool);
+        if (ok && to.pend) ok = tok_store(to, to.p0, to.p1, to.p2, to.p3, pool);
         if (!ok) err = INF_OVERFLOW;
       }
       to.n = 0;
@@ -710,6 +700,546 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_decode(const uint8_t
       status[blk] = err;
       found[blk] = err == INF_OVERFLOW ? 0 : o;  // an overflowed block has no complete token stream
       state = S_NEXT;
+    }
+  }
+}
+
+// ---- wave decoder (fast path) -------------------------------------------------------------------------------
+// One wavefront per BGZF block.  Huffman decoding is inherently serial per block, so the 64 lanes decode 64
+// consecutive kK-bit segments of a deflate block's data at once, each from a guessed start (its segment's first
+// bit, literal/length state); Huffman codes resynchronise within a few symbols, so a lane whose true start (the
+// position where its left neighbour's decode leaves its segment) differs re-decodes from there only until its
+// path meets a symbol boundary of its own first pass (phase B).  Token and byte counts then give every lane its
+// output offset (wave prefix sums), and a second pass (phase C) writes the tokens.  Tables (a 10-bit root table
+// plus sub-tables for longer codes; 8 bits for distances) are built by the whole wave in LDS, so a symbol costs
+// one or two LDS lookups instead of the slow decoder's compare chain.  Anything outside the common case — stored
+// or invalid blocks, incomplete codes, a stream ending before ISIZE or running past it, a distance too far back —
+// sends the block to k_inflate_slow (the exact per-lane decoder), so zlib's semantics are unchanged.
+namespace wd {
+constexpr int kK = 512;                    // bits per lane segment
+constexpr int kWinDw = 64 * kK / 32 + 16;  // staged input dwords per round (start alignment + lookahead)
+constexpr int kLitRoot = 10, kDistRoot = 8;
+constexpr int kLitCap = (1 << kLitRoot) + 320;   // root + sub-tables (zlib's ENOUGH for 286 symbols, root 10: 1332)
+constexpr int kDistCap = (1 << kDistRoot) + 192;  // (ENOUGH for 30 symbols, root 8: 400)
+constexpr int kM = 12;                     // first-pass symbol boundaries a lane records for resynchronisation
+constexpr uint32_t kSub = 1u << 10;        // entry flag: pointer to a sub-table
+enum : uint32_t { K_LIT = 0, K_LEN = 1, K_DIST = 2, K_SPEC = 3 };
+enum : int { ST_NONE = 0, ST_EOB = 1, ST_ERR = 2, ST_OUT = 3 };
+}  // namespace wd
+
+// Table entry: bits 0-3 code length (total; a sub-table pointer holds the root bits), 4-7 extra bits, 8-9 kind,
+// 10 sub-table flag, 11-15 sub-table index bits, 16-31 value (literal byte, length or distance base, sub-table
+// offset; K_SPEC: 0 = end of block, 1 = invalid symbol).
+struct WaveLds {
+  uint32_t win[wd::kWinDw];
+  uint32_t lit[wd::kLitCap];
+  uint32_t dist[wd::kDistCap];
+  uint16_t sorted[320];  // canonical index -> symbol (lit/len [0, 288), distance [288, 320))
+  uint8_t lens[320];     // code lengths (lit/len [0, 288), distance [288, 320))
+  uint8_t cl[128];       // code-length code, 7-bit lookup: length << 5 | symbol
+  uint32_t cnt[16];
+};
+
+SB_DEV uint32_t sym_entry(uint32_t s, uint32_t l, bool dist) {
+  using namespace wd;
+  if (!dist) {
+    if (s < 256) return l | (K_LIT << 8) | (s << 16);
+    if (s == 256) return l | (K_SPEC << 8);
+    if (s <= 285) {
+      const uint32_t k = s - 257;
+      const uint32_t x = (k < 8 || k == 28) ? 0u : (k >> 2) - 1;
+      const uint32_t base = k < 8 ? k + 3 : k == 28 ? 258u : ((4u | (k & 3)) << x) + 3;
+      return l | (x << 4) | (K_LEN << 8) | (base << 16);
+    }
+    return l | (K_SPEC << 8) | (1u << 16);
+  }
+  if (s < 30) {
+    const uint32_t x = s < 4 ? 0u : (s >> 1) - 1;
+    const uint32_t base = s < 4 ? s + 1 : ((2u | (s & 1)) << x) + 1;
+    return l | (x << 4) | (K_DIST << 8) | (base << 16);
+  }
+  return l | (K_SPEC << 8) | (1u << 16);
+}
+
+// Canonical code of one alphabet, wave-uniform: lim[l] = left-justified (15-bit) end of the length-l codes,
+// base[l] = canonical index of the first length-l code minus that code.
+struct CanonW {
+  uint32_t lim[16];
+  int32_t base[16];
+};
+SB_DEV uint32_t canon_len(const CanonW &c, uint32_t v) {  // code length of the 15-bit left-justified code v
+  uint32_t l = 1;
+  sfor<1, 15>([&](auto I) { l += v >= c.lim[decltype(I)::value] ? 1u : 0u; });
+  return l;
+}
+
+SB_DEV uint32_t wave_incl_scan(uint32_t x) {
+  const int lane = (int)threadIdx.x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+// Decode table of one alphabet from lens[off, off + nsym), by the whole wave.  Returns false (wave-uniform) for a
+// code set that is not complete (zlib rejects over-subscribed ones and most incomplete ones; the slow decoder
+// handles every such block exactly) or whose sub-tables would not fit.
+template <bool DIST>
+SB_DEV bool wave_build(WaveLds &L, int off, int nsym, uint32_t *tab, int cap) {
+  constexpr int R = DIST ? wd::kDistRoot : wd::kLitRoot;
+  const int lane = (int)threadIdx.x;
+  if (lane < 16) L.cnt[lane] = 0;
+  __syncthreads();
+  for (int s = lane; s < nsym; s += 64) {
+    const uint32_t l = L.lens[off + s];
+    if (l) atomicAdd(&L.cnt[l], 1u);
+  }
+  __syncthreads();
+  CanonW c;
+  int32_t offs[16];
+  int left = 1, acc = 0;
+  bool over = false;
+  uint32_t code = 0;
+  sfor<1, 16>([&](auto I) {
+    constexpr int l = decltype(I)::value;
+    const uint32_t k = L.cnt[l];
+    left = 2 * left - (int)k;
+    over |= left < 0;
+    c.lim[l] = (code + k) << (15 - l);
+    c.base[l] = acc - (int32_t)code;
+    offs[l] = acc;
+    acc += (int32_t)k;
+    code = (code + k) << 1;
+  });
+  c.lim[0] = 0;
+  c.base[0] = 0;
+  if (over || left != 0) return false;
+  // sorted[canonical index] = symbol: a symbol's rank among the equal-length symbols below it, 64 at a time
+  int32_t run[16];
+  sfor<1, 16>([&](auto I) { run[decltype(I)::value] = 0; });
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (int c0 = 0; c0 < nsym; c0 += 64) {
+    const int s = c0 + lane;
+    const uint32_t l = s < nsym ? L.lens[off + s] : 0u;
+    sfor<1, 16>([&](auto I) {
+      constexpr int ll = decltype(I)::value;
+      const uint64_t m = __ballot(l == (uint32_t)ll);
+      if (l == (uint32_t)ll) L.sorted[off + offs[ll] + run[ll] + __popcll(m & lt)] = (uint16_t)s;
+      run[ll] += __popcll(m);
+    });
+  }
+  __syncthreads();
+  // root entries: stream bits e (LSB first) = code prefix bitrev(e) (MSB first)
+  for (int e = lane; e < (1 << R); e += 64) {
+    const uint32_t v = (__builtin_bitreverse32((uint32_t)e) >> (32 - R)) << (15 - R);
+    if (v < c.lim[R]) {
+      const uint32_t l = canon_len(c, v);
+      const uint32_t sym = L.sorted[off + (int)(v >> (15 - l)) + c.base[l]];
+      tab[e] = sym_entry(sym, l, DIST);
+    }
+  }
+  // sub-tables: one per root prefix of the codes longer than R, sized by the longest code under that prefix
+  const uint32_t P0 = c.lim[R] >> (15 - R);
+  const int npre = (1 << R) - (int)P0;
+  int next = 1 << R;
+  for (int j0 = 0; j0 < npre; j0 += 64) {
+    const int j = j0 + lane;
+    const uint32_t P = P0 + (uint32_t)j;
+    uint32_t sb = 0, sz = 0;
+    if (j < npre) {
+      sb = canon_len(c, ((P + 1) << (15 - R)) - 1) - R;
+      sz = 1u << sb;
+    }
+    const uint32_t incl = wave_incl_scan(sz);
+    const int my = next + (int)(incl - sz);
+    if (j < npre && my + (int)sz <= cap) {
+      tab[__builtin_bitreverse32(P) >> (32 - R)] = (uint32_t)R | wd::kSub | (sb << 11) | ((uint32_t)my << 16);
+      for (uint32_t k = 0; k < sz; k++) {
+        const uint32_t v = (P << (15 - R)) | ((__builtin_bitreverse32(k) >> (32 - sb)) << (15 - R - sb));
+        const uint32_t l = canon_len(c, v);
+        const uint32_t sym = L.sorted[off + (int)(v >> (15 - l)) + c.base[l]];
+        tab[my + (int)k] = sym_entry(sym, l, DIST);
+      }
+    }
+    next += (int)__shfl(incl, 63);
+  }
+  __syncthreads();
+  return next <= cap;
+}
+
+// Per-lane bit reader over the staged window (positions are bits from the block's 16-B aligned base).
+struct WBits {
+  uint64_t bb;
+  int bc, rp, pos;
+  uint32_t nx;
+};
+SB_DEV void wb_init(WBits &r, const uint32_t *win, int wq, int pos) {
+  const int rel = pos - wq, w = rel >> 5, sh = rel & 31;
+  r.bb = ((uint64_t)win[w] | ((uint64_t)win[w + 1] << 32)) >> sh;
+  r.bc = 64 - sh;
+  r.rp = w + 2;
+  r.nx = win[r.rp];
+  r.pos = pos;
+}
+// One symbol of the alphabet `st` selects (literal/length, or distance after a length), with its extra bits.
+SB_DEV uint32_t wb_symbol(WBits &r, const WaveLds &L, int st, uint32_t &v) {
+  const uint32_t lo = (uint32_t)r.bb;
+  const uint32_t *t = st ? L.dist : L.lit;
+  uint32_t e = t[lo & (st ? (1u << wd::kDistRoot) - 1 : (1u << wd::kLitRoot) - 1)];
+  if (e & wd::kSub) e = t[(e >> 16) + ((lo >> (e & 15)) & ((1u << ((e >> 11) & 31)) - 1u))];
+  const uint32_t n = e & 15, x = (e >> 4) & 15, c = n + x;
+  v = (e >> 16) + ((lo >> n) & ((1u << x) - 1u));
+  r.bb >>= c;
+  r.bc -= (int)c;
+  r.pos += (int)c;
+  if (r.bc < 32) {
+    r.bb |= (uint64_t)r.nx << r.bc;
+    r.bc += 32;
+    r.rp++;
+    r.nx = L.win[r.rp];
+  }
+  return e;
+}
+
+// Wave-uniform bit reader for block headers.
+struct HBits {
+  uint64_t bb;
+  int bc, rp, pos;
+  SB_DEV void init(const uint32_t *win, int wq, int p) {
+    const int rel = p - wq, w = rel >> 5, sh = rel & 31;
+    bb = ((uint64_t)win[w] | ((uint64_t)win[w + 1] << 32)) >> sh;
+    bc = 64 - sh;
+    rp = w + 2;
+    pos = p;
+  }
+  SB_DEV void need(const uint32_t *win) {
+    if (bc < 32) {
+      bb |= (uint64_t)win[rp] << bc;
+      bc += 32;
+      rp++;
+    }
+  }
+  SB_DEV uint32_t get(const uint32_t *win, int n) {
+    need(win);
+    const uint32_t v = (uint32_t)bb & ((1u << n) - 1u);
+    bb >>= n;
+    bc -= n;
+    pos += n;
+    return v;
+  }
+};
+
+// Stage kWinDw dwords from dword wq_dw of the block's aligned base into the window (zeros past the buffer).
+SB_DEV void wave_stage(uint32_t *win, const uint32_t *base, int64_t base_dw, int wq_dw, int64_t lim_dw) {
+  const int lane = (int)threadIdx.x;
+  __syncthreads();  // every lane is done with the previous window
+  for (int i = lane * 4; i < wd::kWinDw; i += 256) {
+    const int64_t g = base_dw + wq_dw + i;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (g + 4 <= lim_dw) v = *reinterpret_cast<const uint4 *>(base + wq_dw + i);
+    *reinterpret_cast<uint4 *>(win + i) = v;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(64) void k_inflate_wave(const uint8_t *__restrict__ d, int64_t D, BlockTable bt,
+                                                     uint8_t *__restrict__ pool, int32_t *__restrict__ status,
+                                                     int32_t *__restrict__ found, int32_t *__restrict__ slow,
+                                                     unsigned int *nslow) {
+  using namespace wd;
+  __shared__ __attribute__((aligned(16))) WaveLds L;
+  const int lane = (int)threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const int64_t st0 = bt.start[b];
+  const int32_t hs = bt.hsize[b], cs = bt.csize[b], us = bt.usize[b];
+  const int32_t dlen = cs - hs - 8;  // Stream.scala: dataLength = compressedSize - headerSize - FOOTER_SIZE
+  if (us == 0 || us < 0 || us > 65536 || dlen < 0 || st0 + hs + dlen > D) {
+    if (lane == 0) {
+      status[b] = us == 0 ? INF_OK : INF_DATA;  // inflate(buf, 0, 0) returns 0; else a data error
+      found[b] = 0;
+    }
+    return;
+  }
+  const int64_t a = st0 + hs;
+  const int64_t base_dw = (a >> 4) << 2;  // 16-B aligned dword base of the payload
+  const uint32_t *base = reinterpret_cast<const uint32_t *>(d) + base_dw;
+  const int64_t lim_dw = (D + kCompPad) >> 2;
+  const int skip = (int)(a - base_dw * 4) * 8;
+  const int pend = skip + 8 * dlen;  // payload end (bits)
+  uint8_t *reg = pool + tok_region(bt.uoff[b], b);
+  int pos = skip;
+  int out = 0, ntok = 0;
+  bool ok = true;
+
+  for (bool fin = false; ok && !fin;) {
+    // ---- block header (wave-uniform)
+    int wq = (pos >> 7) << 7;
+    wave_stage(L.win, base, base_dw, wq >> 5, lim_dw);
+    HBits h;
+    h.init(L.win, wq, pos);
+    if (pos + 3 > pend) { ok = false; break; }
+    fin = h.get(L.win, 1) != 0;
+    const uint32_t type = h.get(L.win, 2);
+    int hlit = 288, hdist = 32;
+    if (type == 1) {  // fixed codes: lit 0-143:8, 144-255:9, 256-279:7, 280-287:8; dist 0-31:5
+      for (int i = lane; i < 320; i += 64)
+        L.lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : i < 288 ? 8 : 5;
+    } else if (type == 2) {
+      hlit = (int)h.get(L.win, 5) + 257;
+      hdist = (int)h.get(L.win, 5) + 1;
+      const int hclen = (int)h.get(L.win, 4) + 4;
+      if (hlit > 286 || hdist > 30) { ok = false; break; }
+      uint64_t clp = 0;
+      for (int i = 0; i < 19; i++)
+        if (i < hclen) clp |= (uint64_t)h.get(L.win, 3) << (3 * kClOrder[i]);
+      // code-length code: complete, 7-bit lookup table
+      int left = 1;
+      uint32_t first[8], code = 0;
+      bool over = false;
+#pragma unroll
+      for (int l = 1; l <= 7; l++) {
+        uint32_t k = 0;
+#pragma unroll
+        for (int s2 = 0; s2 < 19; s2++) k += ((clp >> (3 * s2)) & 7) == (uint64_t)l ? 1u : 0u;
+        left = 2 * left - (int)k;
+        over |= left < 0;
+        first[l] = code;
+        code = (code + k) << 1;
+      }
+      if (over || left != 0) { ok = false; break; }
+      if (lane < 19) {
+        const uint32_t l = (uint32_t)(clp >> (3 * lane)) & 7u;
+        if (l) {
+          uint32_t rank = 0;
+          for (int s2 = 0; s2 < lane; s2++) rank += ((clp >> (3 * s2)) & 7) == l ? 1u : 0u;
+          uint32_t fc = 0;
+#pragma unroll
+          for (int ll = 1; ll <= 7; ll++) fc = l == (uint32_t)ll ? first[ll] : fc;
+          const uint32_t r = __builtin_bitreverse32(fc + rank) >> (32 - l);
+          for (uint32_t k = r; k < 128; k += 1u << l) L.cl[k] = (uint8_t)((l << 5) | (uint32_t)lane);
+        }
+      }
+      for (int i = lane; i < 320; i += 64) L.lens[i] = 0;
+      __syncthreads();
+      const int total = hlit + hdist;
+      int n = 0;
+      uint32_t prev = 0;
+      while (n < total) {
+        h.need(L.win);
+        const uint32_t e = L.cl[(uint32_t)h.bb & 127u];
+        const int l = (int)(e >> 5);
+        const uint32_t sym = e & 31u;
+        h.bb >>= l;
+        h.bc -= l;
+        h.pos += l;
+        int rep = 1;
+        uint32_t v = sym;
+        if (sym == 16) {
+          if (n == 0) { ok = false; break; }
+          rep = 3 + (int)h.get(L.win, 2);
+          v = prev;
+        } else if (sym == 17) {
+          rep = 3 + (int)h.get(L.win, 3);
+          v = 0;
+        } else if (sym == 18) {
+          rep = 11 + (int)h.get(L.win, 7);
+          v = 0;
+        }
+        if (n + rep > total || h.pos > pend) { ok = false; break; }
+        if (v)
+          for (int j = lane; j < rep; j += 64) {
+            const int idx = n + j;
+            L.lens[idx < hlit ? idx : 288 + idx - hlit] = (uint8_t)v;
+          }
+        n += rep;
+        prev = v;
+      }
+      if (!ok) break;
+      __syncthreads();
+      if (L.lens[256] == 0) { ok = false; break; }  // no end-of-block code
+    } else {  // stored (rare in BGZF) or invalid: the slow decoder
+      ok = false;
+      break;
+    }
+    if (h.pos > pend) { ok = false; break; }
+    if (!wave_build<true>(L, 288, hdist, L.dist, kDistCap)) { ok = false; break; }
+    if (!wave_build<false>(L, 0, hlit, L.lit, kLitCap)) { ok = false; break; }
+
+    // ---- data rounds: 64 segments of kK bits per round
+    uint32_t S = (uint32_t)h.pos << 10;  // round start: pos << 10 | state << 9 | pending match length
+    for (;;) {
+      const int Sp = (int)(S >> 10);
+      wq = (Sp >> 7) << 7;
+      wave_stage(L.win, base, base_dw, wq >> 5, lim_dw);
+      const int seg_start = lane == 0 ? Sp : Sp + lane * kK;
+      const int seg_end = Sp + (lane + 1) * kK;
+      // phase A: every lane decodes its segment from a guessed start (lane 0: the true one)
+      uint32_t bA[kM], cA[kM];
+      uint32_t tokA = 0, bytA = 0, exitA;
+      int stopA = ST_NONE;
+      {
+        int stt = lane == 0 ? (int)((S >> 9) & 1) : 0;
+        uint32_t pl = lane == 0 ? (S & 511u) : 0u;
+        WBits r;
+        bool done = false;
+        if (seg_start >= pend && lane > 0) {
+          stopA = ST_OUT;
+          done = true;
+          r.pos = seg_start;
+        } else {
+          wb_init(r, L.win, wq, seg_start);
+        }
+        auto step = [&]() {
+          uint32_t v;
+          const uint32_t e = wb_symbol(r, L, stt, v);
+          const uint32_t kind = (e >> 8) & 3;
+          if (r.pos > pend) stopA = ST_OUT;
+          else if (kind == K_SPEC) stopA = v == 0 ? ST_EOB : ST_ERR;
+          else {
+            tokA++;
+            bytA += kind == K_LIT ? 1u : kind == K_LEN ? v : 0u;
+            pl = kind == K_LEN ? v : pl;
+            stt = kind == K_LEN ? 1 : 0;
+          }
+          done = stopA != ST_NONE;
+        };
+        sfor<0, kM>([&](auto I) {
+          constexpr int k = decltype(I)::value;
+          bA[k] = ~0u;
+          cA[k] = 0;
+          if (!done && r.pos < seg_end) {
+            bA[k] = stt == 0 ? (uint32_t)r.pos : ~0u;
+            cA[k] = tokA | (bytA << 12);
+            step();
+          }
+        });
+        while (!done && r.pos < seg_end) step();
+        exitA = ((uint32_t)r.pos << 10) | ((uint32_t)stt << 9) | pl;
+      }
+      // phase B: lanes whose true start differs re-decode until they meet their own first-pass path
+      uint32_t exitk = exitA, tok = tokA, byt = bytA;
+      int stop = stopA;
+      uint32_t bst = lane == 0 ? S : ((uint32_t)seg_start << 10);
+      int f = 64;
+      for (;;) {
+        uint32_t pex = __shfl_up(exitk, 1);
+        if (lane == 0) pex = S;
+        const uint64_t stops = __ballot(stop != ST_NONE);
+        f = stops ? __ffsll((unsigned long long)stops) - 1 : 64;
+        const bool need = lane > 0 && lane <= f && pex != bst;
+        if (__ballot(need) == 0) break;
+        if (need) {
+          int stt = (int)((pex >> 9) & 1);
+          uint32_t pl = pex & 511u, tk = 0, by = 0;
+          WBits r;
+          wb_init(r, L.win, wq, (int)(pex >> 10));
+          int sp = ST_NONE;
+          for (;;) {
+            if (stt == 0) {
+              int hit = -1;
+              uint32_t cj = 0;
+              sfor<0, kM>([&](auto I) {
+                constexpr int k = decltype(I)::value;
+                if (bA[k] == (uint32_t)r.pos) {
+                  hit = k;
+                  cj = cA[k];
+                }
+              });
+              if (hit >= 0) {  // on the first-pass path from here: its exit, stop and remaining counts hold
+                tok = tk + tokA - (cj & 4095u);
+                byt = by + bytA - (cj >> 12);
+                stop = stopA;
+                exitk = exitA;
+                break;
+              }
+            }
+            if (r.pos >= seg_end) {
+              tok = tk;
+              byt = by;
+              stop = ST_NONE;
+              exitk = ((uint32_t)r.pos << 10) | ((uint32_t)stt << 9) | pl;
+              break;
+            }
+            uint32_t v;
+            const uint32_t e = wb_symbol(r, L, stt, v);
+            const uint32_t kind = (e >> 8) & 3;
+            if (r.pos > pend) sp = ST_OUT;
+            else if (kind == K_SPEC) sp = v == 0 ? ST_EOB : ST_ERR;
+            if (sp != ST_NONE) {
+              tok = tk;
+              byt = by;
+              stop = sp;
+              exitk = ((uint32_t)r.pos << 10) | ((uint32_t)stt << 9) | pl;
+              break;
+            }
+            tk++;
+            by += kind == K_LIT ? 1u : kind == K_LEN ? v : 0u;
+            pl = kind == K_LEN ? v : pl;
+            stt = kind == K_LEN ? 1 : 0;
+          }
+          bst = pex;
+        }
+      }
+      // lanes 0..f carry the true path (f: the lane whose segment ends the deflate block, or 64)
+      const bool act = lane <= f;
+      const uint32_t my_tok = act ? tok : 0u, my_byt = act ? byt : 0u;
+      const uint32_t itok = wave_incl_scan(my_tok), ibyt = wave_incl_scan(my_byt);
+      const uint32_t tot_tok = __shfl(itok, 63), tot_byt = __shfl(ibyt, 63);
+      const int stop_f = f < 64 ? __shfl(stop, f) : ST_NONE;
+      if (stop_f == ST_ERR || stop_f == ST_OUT || out + (int)tot_byt > us) { ok = false; break; }
+      // phase C: decode the true segments again, writing tokens at their offsets
+      bool derr = false;
+      if (act) {
+        uint32_t start = __shfl_up(exitk, 1);
+        if (lane == 0) start = S;
+        int stt = (int)((start >> 9) & 1);
+        uint32_t pl = start & 511u;
+        WBits r;
+        wb_init(r, L.win, wq, (int)(start >> 10));
+        int o = out + (int)(ibyt - my_byt);
+        uint32_t ti = (uint32_t)ntok + (itok - my_tok), hold = 0;
+        bool has = false;
+        while (r.pos < seg_end) {
+          uint32_t v;
+          const uint32_t e = wb_symbol(r, L, stt, v);
+          const uint32_t kind = (e >> 8) & 3;
+          if (kind == K_SPEC) break;  // the end-of-block symbol of lane f
+          const uint32_t t = kind == K_LIT ? v : kind == K_LEN ? v + 253u : v - 1u;
+          if (kind == K_DIST) derr |= (int)v > o - (int)pl;
+          o += kind == K_LIT ? 1 : kind == K_LEN ? (int)v : 0;
+          pl = kind == K_LEN ? v : pl;
+          stt = kind == K_LEN ? 1 : 0;
+          if (ti & 1u) {
+            if (has) *reinterpret_cast<uint32_t *>(reg + 2 * (ti - 1)) = hold | (t << 16);
+            else *reinterpret_cast<uint16_t *>(reg + 2 * ti) = (uint16_t)t;
+            has = false;
+          } else {
+            hold = t;
+            has = true;
+          }
+          ti++;
+        }
+        if (has) *reinterpret_cast<uint16_t *>(reg + 2 * (ti - 1)) = (uint16_t)hold;
+      }
+      if (__ballot(derr) != 0) { ok = false; break; }
+      out += (int)tot_byt;
+      ntok += (int)tot_tok;
+      if (f < 64) {  // end of block: the next header follows lane f's end-of-block symbol
+        pos = (int)(__shfl(exitk, f) >> 10);
+        break;
+      }
+      S = __shfl(exitk, 63);
+    }
+  }
+  if (ok && out != us) ok = false;
+  if (lane == 0) {
+    if (ok) {
+      status[b] = INF_OK;
+      found[b] = us;
+    } else {
+      slow[atomicAdd(nslow, 1u)] = (int32_t)b;
     }
   }
 }
@@ -733,19 +1263,17 @@ constexpr int kResLits = 4;  // literals a step may take (the first token plus u
 static_assert(63 + 16 <= kNear + 1, "far copies read only flushed output");
 static_assert(kNear + 16 + kResLits + 3 <= 128, "a step's ring writes never reach the near window");
 
-// Tokens are read a group of kTokGroupChunks 16-B chunks at a time (aligned; a page's first group starts with
-// the next-page link).
+// Tokens are read a group of kTG 16-B chunks at a time from the block's (16-B aligned) token region.
 constexpr int kTokGroup = 128;
 constexpr int kTG = kTokGroup / 16;  // chunks per token group
-static_assert(kTG >= 2 && (kTokPage % kTokGroup) == 0, "token groups tile a page");
+static_assert(kTG >= 2, "a group holds the current chunk and at least one more");
 
 struct TokIn {
   uint32_t t0, t1, t2, t3;      // current chunk (t0 low half = next token)
   uint32_t q[4 * (kTG - 1)];    // up to kTG - 1 more chunks
   int n;                        // tokens left in t0..t3
   int nq;                       // chunks left in q
-  uint64_t cur;                 // byte offset of the next group in the pool
-  uint32_t pnext;               // next page of this block
+  uint64_t cur;                 // byte offset of the next group in the token buffer
   SB_DEV void load(const uint8_t *pool) {
     const uint4 *g = reinterpret_cast<const uint4 *>(pool + cur);
     uint4 c[kTG];
@@ -756,16 +1284,9 @@ struct TokIn {
       q[4 * (k - 1) + 0] = c[k].x; q[4 * (k - 1) + 1] = c[k].y;
       q[4 * (k - 1) + 2] = c[k].z; q[4 * (k - 1) + 3] = c[k].w;
     }
-    if ((cur & (kTokPage - 1)) == 0) {  // a page's first group: chunk 0 links to the next page
-      pnext = c[0].x;
-      t0 = t1 = t2 = t3 = 0;
-      nq = kTG - 1;
-    } else {
-      t0 = c[0].x; t1 = c[0].y; t2 = c[0].z; t3 = c[0].w;
-      nq = kTG;  // (t counts as the first)
-    }
+    t0 = c[0].x; t1 = c[0].y; t2 = c[0].z; t3 = c[0].w;
+    nq = kTG;  // (t counts as the first)
     cur += 16 * kTG;
-    if ((cur & (kTokPage - 1)) == 0) cur = (uint64_t)pnext * kTokPage;
   }
   SB_DEV uint32_t get(const uint8_t *pool) {
     if (n == 0) {
@@ -792,7 +1313,6 @@ struct TokIn {
 
 __global__ __launch_bounds__(kResThreads, 4) void k_inflate_resolve(BlockTable bt, uint8_t *__restrict__ out,
                                                                     const uint8_t *__restrict__ pool,
-                                                                    const int32_t *__restrict__ blk_page,
                                                                     const int32_t *__restrict__ found,
                                                                     unsigned int *next_block) {
   __shared__ __attribute__((aligned(16))) uint8_t s_ring[kResThreads * kResRing];
@@ -809,7 +1329,6 @@ __global__ __launch_bounds__(kResThreads, 4) void k_inflate_resolve(BlockTable b
   for (int k = 0; k < 4 * (kTG - 1); k++) ti.q[k] = 0;
   ti.n = ti.nq = 0;
   ti.cur = 0;
-  ti.pnext = 0;
   int crem = 0, eff = 0, npad = 0;
   auto flush16 = [&](int64_t x) {  // the aligned 16-B chunk at x (ring stride is 8-B aligned)
     const uint2 lo = *reinterpret_cast<const uint2 *>(ring + (x & 127));
@@ -824,13 +1343,12 @@ __global__ __launch_bounds__(kResThreads, 4) void k_inflate_resolve(BlockTable b
         exited = true;
       } else {
         const int32_t f = found[b];
-        const int32_t pg = blk_page[b];
-        if (f > 0 && pg >= 0) {
+        if (f > 0) {
           a = bt.uoff[b];
           ae = a + f;
           fl = a;
           ti.n = ti.nq = 0;
-          ti.cur = (uint64_t)pg * kTokPage;
+          ti.cur = tok_region(bt.uoff[b], b);
           crem = 0;
           npad = 0;
           active = true;
@@ -961,22 +1479,23 @@ hipError_t launch_first_error(const int32_t *status, int64_t n, unsigned long lo
 }
 
 
-hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *pool, uint32_t npages,
-                                 int32_t *blk_page, int32_t *status, int32_t *found, unsigned int *counters,
-                                 int dec_wgs, hipStream_t s) {
+hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *tok, int32_t *status,
+                                 int32_t *found, int32_t *slow, unsigned int *counters, hipStream_t s) {
   if (bt.n == 0) return hipSuccess;
-  // counters: [0] decode work, [1] pool pages used, [2] resolve work
+  // counters: [0] slow-path blocks, [1] slow-path work, [2] resolve work
   (void)hipMemsetAsync(counters, 0, 3 * sizeof(unsigned int), s);
-  hipLaunchKernelGGL(k_inflate_decode, dim3((unsigned)dec_wgs), dim3(kDecThreads), 0, s, d, D, bt, pool, npages,
-                     counters + 1, blk_page, status, found, counters + 0);
+  hipLaunchKernelGGL(k_inflate_wave, dim3((unsigned)bt.n), dim3(64), 0, s, d, D, bt, tok, status, found, slow,
+                     counters + 0);
+  hipLaunchKernelGGL(k_inflate_slow, dim3(256), dim3(kDecThreads), 0, s, d, D, bt, tok, slow, counters + 0, status,
+                     found, counters + 1);
   return hipGetLastError();
 }
 
-hipError_t launch_inflate_resolve(BlockTable bt, uint8_t *out, const uint8_t *pool, const int32_t *blk_page,
-                                  const int32_t *found, unsigned int *counters, int res_wgs, hipStream_t s) {
+hipError_t launch_inflate_resolve(BlockTable bt, uint8_t *out, const uint8_t *tok, const int32_t *found,
+                                  unsigned int *counters, int res_wgs, hipStream_t s) {
   if (bt.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_inflate_resolve, dim3((unsigned)res_wgs), dim3(kResThreads), 0, s, bt, out, pool, blk_page,
-                     found, counters + 2);
+  hipLaunchKernelGGL(k_inflate_resolve, dim3((unsigned)res_wgs), dim3(kResThreads), 0, s, bt, out, tok, found,
+                     counters + 2);
   return hipGetLastError();
 }
 

@@ -55,7 +55,6 @@ struct RecordColumnsDev {
 constexpr int kScanChunk = 1 << 20;  // bytes per workgroup in the BGZF candidate scan
 constexpr int kStreamPad = 16384;  // zero pad behind the uncompressed stream (>= checker LDS window)
 constexpr int kCompPad = 256;  // zero pad behind the compressed bytes (bit-reader / input-ring lookahead)
-constexpr uint64_t kTokPage = 4096;  // inflate token page: 16-B header (next page) + 255 chunks of 8 u16 tokens
 
 hipError_t launch_scan_count(const uint8_t *d, int64_t D, int32_t *chunk_counts, int64_t nchunks, hipStream_t s);
 hipError_t launch_scan_prefix(int32_t *chunk_counts, int64_t nchunks, int64_t *chunk_offsets, int64_t *total,
@@ -69,13 +68,16 @@ hipError_t launch_find_block_starts(const uint8_t *d, int64_t D, const Candidate
                                     hipStream_t s);
 hipError_t launch_gather_blocks(const Candidate *cands, int64_t first, int64_t n, int64_t *start, int32_t *hsize,
                                 int32_t *csize, int32_t *usize, hipStream_t s);
-// Two-kernel inflate (sbam_inflate.hip): entropy decode into token pages, then LZ77 resolve into `out`.
-// counters: 3 × u32 device scratch (decode work, pool pages used, resolve work), reset by the decode launch.
-hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *pool, uint32_t npages,
-                                 int32_t *blk_page, int32_t *status, int32_t *found, unsigned int *counters,
-                                 int dec_wgs, hipStream_t s);
-hipError_t launch_inflate_resolve(BlockTable bt, uint8_t *out, const uint8_t *pool, const int32_t *blk_page,
-                                  const int32_t *found, unsigned int *counters, int res_wgs, hipStream_t s);
+// Inflate (sbam_inflate.hip): entropy decode into per-block token regions (wave-parallel fast path, per-lane
+// exact path for the blocks it hands over), then LZ77 resolve into `out`.  tok: inflate_token_bytes(L, nb) bytes;
+// slow: nb int32; counters: 3 × u32 device scratch, reset by the decode launch.
+inline size_t inflate_token_bytes(int64_t L, int64_t nb) {
+  return ((2 * (size_t)L + 15) & ~(size_t)15) + 32 * (size_t)nb + 256;
+}
+hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *tok, int32_t *status,
+                                 int32_t *found, int32_t *slow, unsigned int *counters, hipStream_t s);
+hipError_t launch_inflate_resolve(BlockTable bt, uint8_t *out, const uint8_t *tok, const int32_t *found,
+                                  unsigned int *counters, int res_wgs, hipStream_t s);
 // first_err = min block index with status != 0 (caller presets ~0)
 hipError_t launch_first_error(const int32_t *status, int64_t n, unsigned long long *first_err, hipStream_t s);
 hipError_t launch_lower_bound(const Candidate *c, int64_t n, int64_t q, int64_t *out, hipStream_t s);

@@ -111,7 +111,7 @@ RECORD_COLUMNS = {"offset": np.int64, "block_pos": np.int64, "block_off": np.int
 
 EXPORTS = [  # every symbol include/sbam.h declares
     "sbam_open", "sbam_close", "sbam_load", "sbam_last_error", "sbam_set_path", "sbam_reset", "sbam_version", "sbam_find_block_starts", "sbam_scan_blocks",
-    "sbam_get_blocks", "sbam_inflate", "sbam_read_uncompressed", "sbam_pos_to_offset", "sbam_offset_to_pos",
+    "sbam_get_blocks", "sbam_inflate", "sbam_inflate_fallbacks", "sbam_read_uncompressed", "sbam_pos_to_offset", "sbam_offset_to_pos",
     "sbam_header", "sbam_set_contig_lengths", "sbam_check_eager", "sbam_check_full_words", "sbam_check_full_counts",
     "sbam_find_record_start", "sbam_file_splits", "sbam_split_records", "sbam_compute_splits",
     "sbam_record_offsets", "sbam_record_spans", "sbam_load_records", "sbam_get_record_columns", "sbam_record_columns_device",
@@ -154,6 +154,7 @@ def load_library(path: str = LIB_PATH):
         "sbam_scan_blocks": (ctypes.c_int, [vp, P(i64)]),
         "sbam_get_blocks": (ctypes.c_int, [vp, vp, vp, vp, vp, i64]),
         "sbam_inflate": (ctypes.c_int, [vp, P(i64)]),
+        "sbam_inflate_fallbacks": (ctypes.c_int, [vp, P(i64)]),
         "sbam_read_uncompressed": (ctypes.c_int, [vp, i64, i64, vp]),
         "sbam_pos_to_offset": (ctypes.c_int, [vp, _Pos, P(i64)]),
         "sbam_offset_to_pos": (ctypes.c_int, [vp, i64, P(_Pos)]),
@@ -362,6 +363,12 @@ class BamFile:
         n = ctypes.c_int64(0)
         self._check(self.L.sbam_inflate(self.ctx, ctypes.byref(n)))
         self.uncompressed_size = n.value
+        return n.value
+
+    def inflate_fallbacks(self) -> int:
+        """Blocks the last inflate decoded on the exact per-lane path instead of the wave-parallel one."""
+        n = ctypes.c_int64(0)
+        self._check(self.L.sbam_inflate_fallbacks(self.ctx, ctypes.byref(n)))
         return n.value
 
     def read_uncompressed(self, off: int, length: int) -> bytes:

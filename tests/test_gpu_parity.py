@@ -29,6 +29,13 @@ def test_inflate_bytes(name, gpu_files, oracle_files):
 
 
 @pytest.mark.parametrize("name", ALL_BAMS)
+def test_wave_decoder_covers_fixture_blocks(name, gpu_files):
+    """Every block of the reference's BAMs (htsjdk/zlib dynamic-Huffman streams) is decoded by the wave-parallel
+    decoder; none needs the exact per-lane fallback."""
+    assert gpu_files(name).inflate_fallbacks() == 0
+
+
+@pytest.mark.parametrize("name", ALL_BAMS)
 def test_header(name, gpu_files, oracle_files):
     g, o = gpu_files(name), oracle_files(name)
     assert g.n_ref == o.nref

@@ -118,3 +118,19 @@ def test_inflate_mis_sized_isize(seed):
 def test_inflate_corrupted_payloads(seed):
     data = build_file(seed, corrupt=1 + seed % 4)
     assert gpu_result(data) == oracle_result(data)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(4))
+def test_wave_decoder_takes_every_compressed_block(seed):
+    """Only the stored (level 0) blocks go to the per-lane fallback; fixed, dynamic, Huffman-only and RLE blocks
+    are decoded by the wave-parallel decoder (whose output test_inflate_shapes_bit_exact checks)."""
+    import sbam
+    data = build_file(seed)
+    stored = sum(1 for i in range(len(sample_inputs(seed))) if SHAPES[(i + seed) % len(SHAPES)][0] == 0)
+    g = sbam.BamFile(data, inflate=False)
+    try:
+        g.inflate()
+        assert g.inflate_fallbacks() == stored
+    finally:
+        g.close()

@@ -31,6 +31,7 @@ def test_synthetic_every_offset_and_counts(synth_file):
     with sbam.BamFile(data, path="synth.bam") as g:
         assert g.uncompressed_size == o.L
         assert g.read_uncompressed(0, o.L) == o.u[:o.L].tobytes()
+        assert g.inflate_fallbacks() == 0  # every block through the wave-parallel decoder
         w = o.check_full_range(0, o.L)
         got = g.check_full_words(0, o.L)
         bad = np.flatnonzero(got != w)
