@@ -705,39 +705,47 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
 }
 
 // ---- wave decoder (fast path) -------------------------------------------------------------------------------
-// One wavefront per BGZF block.  Huffman decoding is inherently serial per block, so the 64 lanes decode 64
-// consecutive kK-bit segments of a deflate block's data at once, each from a guessed start (its segment's first
-// bit, literal/length state); Huffman codes resynchronise within a few symbols, so a lane whose true start (the
-// position where its left neighbour's decode leaves its segment) differs re-decodes from there only until its
-// path meets a symbol boundary of its own first pass (phase B).  Token and byte counts then give every lane its
-// output offset (wave prefix sums), and a second pass (phase C) writes the tokens.  Tables (a 10-bit root table
-// plus sub-tables for longer codes; 8 bits for distances) are built by the whole wave in LDS, so a symbol costs
-// one or two LDS lookups instead of the slow decoder's compare chain.  Anything outside the common case — stored
-// or invalid blocks, incomplete codes, a stream ending before ISIZE or running past it, a distance too far back —
-// sends the block to k_inflate_slow (the exact per-lane decoder), so zlib's semantics are unchanged.
+// One wavefront per BGZF block.  Huffman decoding is serial per stream, so the 64 lanes decode 64 consecutive
+// kK-bit segments of a deflate block's data at once, each from a guessed start (its segment's first bit, in the
+// literal/length state).  Huffman codes resynchronise within a few symbols: a lane whose true start (where its
+// left neighbour's decode leaves that neighbour's segment) differs re-decodes from there (phase B) only until
+// its path reaches one of the checkpoints its first pass (phase A) recorded every kCpSteps symbols, after which the
+// first pass's counts hold.  Token and byte counts give every lane its output offset (wave prefix sums), and a
+// second pass over the true segments (phase C) writes the tokens.  A first pass does not stop at an
+// end-of-block or invalid symbol (in the speculative prefix such a symbol is noise): it records up to two such
+// stops and keeps decoding, and phase B decides which, if any, lies on the true path.
+// Block headers are decoded by the whole wave as well: every lane decodes the code-length symbol at one of 64
+// consecutive bit offsets, and the true chain of symbols is followed through those 64 results.  Tables (16-bit
+// entries: a 10-bit root table plus sub-tables for longer codes; 8 bits for distances) are built by the whole
+// wave in LDS.  Anything outside the common case — stored or invalid blocks, incomplete codes, a stream that
+// ends before ISIZE or runs past it, a distance too far back — sends the block to k_inflate_slow (the exact
+// per-lane decoder), so zlib's semantics are unchanged.
 namespace wd {
 constexpr int kK = 512;                    // bits per lane segment
 constexpr int kWinDw = 64 * kK / 32 + 16;  // staged input dwords per round (start alignment + lookahead)
 constexpr int kLitRoot = 10, kDistRoot = 8;
-constexpr int kLitCap = (1 << kLitRoot) + 320;   // root + sub-tables (zlib's ENOUGH for 286 symbols, root 10: 1332)
-constexpr int kDistCap = (1 << kDistRoot) + 192;  // (ENOUGH for 30 symbols, root 8: 400)
-constexpr int kM = 12;                     // first-pass symbol boundaries a lane records for resynchronisation
-constexpr uint32_t kSub = 1u << 10;        // entry flag: pointer to a sub-table
+constexpr int kLitSub = 320, kDistSub = 192;  // zlib's ENOUGH: 1332 for 286 symbols at root 10, 400 for 30 at 8
+constexpr int kLitOff = 0, kDistOff = (1 << kLitRoot) + kLitSub;
+constexpr int kTab = kDistOff + (1 << kDistRoot) + kDistSub;
+constexpr int kCp = 12;            // checkpoints per lane
+constexpr int kCpSteps = 8;        // symbols between checkpoints
+constexpr int kScratchDw = 256;    // window tail that doubles as header / table-build scratch
+constexpr uint32_t kSub = 1u << 10;  // table entry flag: pointer to a sub-table
+// a block header (<= 3 + 14 + 57 + 320 * 14 bits) plus the window's start alignment fits before the scratch
+static_assert(128 + 3 + 14 + 57 + 320 * 14 + 64 <= (kWinDw - kScratchDw) * 32, "header fits the window");
 enum : uint32_t { K_LIT = 0, K_LEN = 1, K_DIST = 2, K_SPEC = 3 };
 enum : int { ST_NONE = 0, ST_EOB = 1, ST_ERR = 2, ST_OUT = 3 };
 }  // namespace wd
 
-// Table entry: bits 0-3 code length (total; a sub-table pointer holds the root bits), 4-7 extra bits, 8-9 kind,
-// 10 sub-table flag, 11-15 sub-table index bits, 16-31 value (literal byte, length or distance base, sub-table
-// offset; K_SPEC: 0 = end of block, 1 = invalid symbol).
+// Table entry (u32): bits 0-3 code length, 4-7 extra bits, 8-9 kind, 10 sub-table flag, 11-15 sub-table index
+// bits, 16-31 value (literal byte, length or distance base; K_SPEC: 0 = end of block, 1 = invalid symbol; for a
+// sub-table pointer: the sub-table's offset in the alphabet's table).
 struct WaveLds {
   uint32_t win[wd::kWinDw];
-  uint32_t lit[wd::kLitCap];
-  uint32_t dist[wd::kDistCap];
-  uint16_t sorted[320];  // canonical index -> symbol (lit/len [0, 288), distance [288, 320))
-  uint8_t lens[320];     // code lengths (lit/len [0, 288), distance [288, 320))
-  uint8_t cl[128];       // code-length code, 7-bit lookup: length << 5 | symbol
+  uint32_t tab[wd::kTab];
   uint32_t cnt[16];
+  SB_DEV uint8_t *lens() { return reinterpret_cast<uint8_t *>(win + wd::kWinDw - wd::kScratchDw); }  // [320]
+  SB_DEV uint16_t *sorted() { return reinterpret_cast<uint16_t *>(win + wd::kWinDw - wd::kScratchDw + 80); }  // [320]
 };
 
 SB_DEV uint32_t sym_entry(uint32_t s, uint32_t l, bool dist) {
@@ -772,6 +780,17 @@ SB_DEV uint32_t canon_len(const CanonW &c, uint32_t v) {  // code length of the 
   sfor<1, 15>([&](auto I) { l += v >= c.lim[decltype(I)::value] ? 1u : 0u; });
   return l;
 }
+SB_DEV int32_t canon_base(const CanonW &c, uint32_t l) {  // c.base[l] by selects (a runtime index would
+  int32_t r = 0;                                            // move the whole struct to scratch memory)
+  sfor<1, 16>([&](auto I) { r = l == (uint32_t)decltype(I)::value ? c.base[decltype(I)::value] : r; });
+  return r;
+}
+
+// Wave-uniform values pinned to scalar registers, so the compiler emits uniform (scalar) control flow instead of
+// exec-mask bookkeeping for branches that never diverge.
+SB_DEV uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+SB_DEV int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+SB_DEV uint64_t uni(uint64_t x) { return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x); }
 
 SB_DEV uint32_t wave_incl_scan(uint32_t x) {
   const int lane = (int)threadIdx.x;
@@ -783,17 +802,20 @@ SB_DEV uint32_t wave_incl_scan(uint32_t x) {
   return x;
 }
 
-// Decode table of one alphabet from lens[off, off + nsym), by the whole wave.  Returns false (wave-uniform) for a
-// code set that is not complete (zlib rejects over-subscribed ones and most incomplete ones; the slow decoder
-// handles every such block exactly) or whose sub-tables would not fit.
+// Decode table of one alphabet from lens[off, off + nsym), by the whole wave, into tab[toff, ...).  Returns false
+// (wave-uniform) for a code set that is not complete (zlib rejects over-subscribed ones and most incomplete ones;
+// the slow decoder handles every such block exactly) or whose sub-tables would not fit.
 template <bool DIST>
-SB_DEV bool wave_build(WaveLds &L, int off, int nsym, uint32_t *tab, int cap) {
+SB_DEV bool wave_build(WaveLds &L, int off, int nsym, int toff, int subcap) {
   constexpr int R = DIST ? wd::kDistRoot : wd::kLitRoot;
   const int lane = (int)threadIdx.x;
+  uint8_t *lens = L.lens();
+  uint16_t *sorted = L.sorted();
+  uint32_t *tab = L.tab + toff;
   if (lane < 16) L.cnt[lane] = 0;
   __syncthreads();
   for (int s = lane; s < nsym; s += 64) {
-    const uint32_t l = L.lens[off + s];
+    const uint32_t l = lens[off + s];
     if (l) atomicAdd(&L.cnt[l], 1u);
   }
   __syncthreads();
@@ -804,7 +826,7 @@ SB_DEV bool wave_build(WaveLds &L, int off, int nsym, uint32_t *tab, int cap) {
   uint32_t code = 0;
   sfor<1, 16>([&](auto I) {
     constexpr int l = decltype(I)::value;
-    const uint32_t k = L.cnt[l];
+    const uint32_t k = uni(L.cnt[l]);
     left = 2 * left - (int)k;
     over |= left < 0;
     c.lim[l] = (code + k) << (15 - l);
@@ -822,11 +844,11 @@ SB_DEV bool wave_build(WaveLds &L, int off, int nsym, uint32_t *tab, int cap) {
   const uint64_t lt = (1ull << lane) - 1ull;
   for (int c0 = 0; c0 < nsym; c0 += 64) {
     const int s = c0 + lane;
-    const uint32_t l = s < nsym ? L.lens[off + s] : 0u;
+    const uint32_t l = s < nsym ? lens[off + s] : 0u;
     sfor<1, 16>([&](auto I) {
       constexpr int ll = decltype(I)::value;
       const uint64_t m = __ballot(l == (uint32_t)ll);
-      if (l == (uint32_t)ll) L.sorted[off + offs[ll] + run[ll] + __popcll(m & lt)] = (uint16_t)s;
+      if (l == (uint32_t)ll) sorted[off + offs[ll] + run[ll] + __popcll(m & lt)] = (uint16_t)s;
       run[ll] += __popcll(m);
     });
   }
@@ -836,14 +858,13 @@ SB_DEV bool wave_build(WaveLds &L, int off, int nsym, uint32_t *tab, int cap) {
     const uint32_t v = (__builtin_bitreverse32((uint32_t)e) >> (32 - R)) << (15 - R);
     if (v < c.lim[R]) {
       const uint32_t l = canon_len(c, v);
-      const uint32_t sym = L.sorted[off + (int)(v >> (15 - l)) + c.base[l]];
-      tab[e] = sym_entry(sym, l, DIST);
+      tab[e] = sym_entry(sorted[off + (int)(v >> (15 - l)) + canon_base(c, l)], l, DIST);
     }
   }
   // sub-tables: one per root prefix of the codes longer than R, sized by the longest code under that prefix
   const uint32_t P0 = c.lim[R] >> (15 - R);
   const int npre = (1 << R) - (int)P0;
-  int next = 1 << R;
+  int next = 0;
   for (int j0 = 0; j0 < npre; j0 += 64) {
     const int j = j0 + lane;
     const uint32_t P = P0 + (uint32_t)j;
@@ -854,52 +875,35 @@ SB_DEV bool wave_build(WaveLds &L, int off, int nsym, uint32_t *tab, int cap) {
     }
     const uint32_t incl = wave_incl_scan(sz);
     const int my = next + (int)(incl - sz);
-    if (j < npre && my + (int)sz <= cap) {
-      tab[__builtin_bitreverse32(P) >> (32 - R)] = (uint32_t)R | wd::kSub | (sb << 11) | ((uint32_t)my << 16);
+    if (j < npre && my + (int)sz <= subcap) {
+      tab[__builtin_bitreverse32(P) >> (32 - R)] = wd::kSub | (sb << 11) | ((uint32_t)((1 << R) + my) << 16);
       for (uint32_t k = 0; k < sz; k++) {
         const uint32_t v = (P << (15 - R)) | ((__builtin_bitreverse32(k) >> (32 - sb)) << (15 - R - sb));
         const uint32_t l = canon_len(c, v);
-        const uint32_t sym = L.sorted[off + (int)(v >> (15 - l)) + c.base[l]];
-        tab[my + (int)k] = sym_entry(sym, l, DIST);
+        tab[(1 << R) + my + (int)k] = sym_entry(sorted[off + (int)(v >> (15 - l)) + canon_base(c, l)], l, DIST);
       }
     }
     next += (int)__shfl(incl, 63);
   }
   __syncthreads();
-  return next <= cap;
+  return next <= subcap;
 }
 
-// Per-lane bit reader over the staged window (positions are bits from the block's 16-B aligned base).
-struct WBits {
-  uint64_t bb;
-  int bc, rp, pos;
-  uint32_t nx;
-};
-SB_DEV void wb_init(WBits &r, const uint32_t *win, int wq, int pos) {
-  const int rel = pos - wq, w = rel >> 5, sh = rel & 31;
-  r.bb = ((uint64_t)win[w] | ((uint64_t)win[w + 1] << 32)) >> sh;
-  r.bc = 64 - sh;
-  r.rp = w + 2;
-  r.nx = win[r.rp];
-  r.pos = pos;
-}
-// One symbol of the alphabet `st` selects (literal/length, or distance after a length), with its extra bits.
-SB_DEV uint32_t wb_symbol(WBits &r, const WaveLds &L, int st, uint32_t &v) {
-  const uint32_t lo = (uint32_t)r.bb;
-  const uint32_t *t = st ? L.dist : L.lit;
-  uint32_t e = t[lo & (st ? (1u << wd::kDistRoot) - 1 : (1u << wd::kLitRoot) - 1)];
-  if (e & wd::kSub) e = t[(e >> 16) + ((lo >> (e & 15)) & ((1u << ((e >> 11) & 31)) - 1u))];
-  const uint32_t n = e & 15, x = (e >> 4) & 15, c = n + x;
-  v = (e >> 16) + ((lo >> n) & ((1u << x) - 1u));
-  r.bb >>= c;
-  r.bc -= (int)c;
-  r.pos += (int)c;
-  if (r.bc < 32) {
-    r.bb |= (uint64_t)r.nx << r.bc;
-    r.bc += 32;
-    r.rp++;
-    r.nx = L.win[r.rp];
-  }
+// One symbol of the alphabet `st` selects (literal/length, or distance after a length) at bit position pos of the
+// staged window (positions are bits from the block's 16-B aligned base; wq = the window's first bit): 32 bits of
+// lookahead from two window dwords, the root entry, the sub-table entry for long codes, the extra bits.  Advances
+// pos; returns the entry, v = literal byte, length, distance or K_SPEC value.
+SB_DEV uint32_t wsym(const WaveLds &L, int wq, int &pos, int st, uint32_t &v) {
+  using namespace wd;
+  const uint32_t q = (uint32_t)(pos - wq), w = q >> 5;
+  const uint32_t lo = __builtin_amdgcn_alignbit(L.win[w + 1], L.win[w], q & 31u);
+  const uint32_t tb = st ? (uint32_t)kDistOff : (uint32_t)kLitOff;
+  const uint32_t R = st ? (uint32_t)kDistRoot : (uint32_t)kLitRoot;
+  uint32_t e = L.tab[tb + (lo & ((1u << R) - 1u))];
+  if (e & kSub) e = L.tab[tb + (e >> 16) + ((lo >> R) & ((1u << ((e >> 11) & 31u)) - 1u))];
+  const uint32_t n = e & 15u, x = (e >> 4) & 15u;
+  v = (e >> 16) + __builtin_amdgcn_ubfe(lo, n, x);
+  pos += (int)(n + x);
   return e;
 }
 
@@ -909,20 +913,17 @@ struct HBits {
   int bc, rp, pos;
   SB_DEV void init(const uint32_t *win, int wq, int p) {
     const int rel = p - wq, w = rel >> 5, sh = rel & 31;
-    bb = ((uint64_t)win[w] | ((uint64_t)win[w + 1] << 32)) >> sh;
+    bb = (((uint64_t)uni(win[w]) | ((uint64_t)uni(win[w + 1]) << 32)) >> sh);
     bc = 64 - sh;
     rp = w + 2;
     pos = p;
   }
-  SB_DEV void need(const uint32_t *win) {
+  SB_DEV uint32_t get(const uint32_t *win, int n) {
     if (bc < 32) {
-      bb |= (uint64_t)win[rp] << bc;
+      bb |= (uint64_t)uni(win[rp]) << bc;
       bc += 32;
       rp++;
     }
-  }
-  SB_DEV uint32_t get(const uint32_t *win, int n) {
-    need(win);
     const uint32_t v = (uint32_t)bb & ((1u << n) - 1u);
     bb >>= n;
     bc -= n;
@@ -944,7 +945,32 @@ SB_DEV void wave_stage(uint32_t *win, const uint32_t *base, int64_t base_dw, int
   __syncthreads();
 }
 
-__global__ __launch_bounds__(64) void k_inflate_wave(const uint8_t *__restrict__ d, int64_t D, BlockTable bt,
+// Result of one lane's decode of its segment from a given start: counts, exit key (pos << 10 | state << 9 |
+// pending length) and stop.
+struct SegResult {
+  uint32_t tok, byt, exit;
+  int stop;
+  bool bad;
+};
+
+#ifdef SBAM_WAVE_STATS
+__device__ unsigned long long g_wave_stats[16];
+#define WMARK(slot) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); ws_[slot] += t_ - wt_; wt_ = t_; } while (0)
+#define WADD(slot, v) ws_[slot] += (v)
+extern "C" int sbam_debug_wave_stats(unsigned long long *out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_stats), sizeof(g_wave_stats)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_wave_stats), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#else
+#define WMARK(slot) do {} while (0)
+#define WADD(slot, v) do {} while (0)
+#endif
+
+__global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restrict__ d, int64_t D, BlockTable bt,
                                                      uint8_t *__restrict__ pool, int32_t *__restrict__ status,
                                                      int32_t *__restrict__ found, int32_t *__restrict__ slow,
                                                      unsigned int *nslow) {
@@ -969,23 +995,30 @@ __global__ __launch_bounds__(64) void k_inflate_wave(const uint8_t *__restrict__
   const int skip = (int)(a - base_dw * 4) * 8;
   const int pend = skip + 8 * dlen;  // payload end (bits)
   uint8_t *reg = pool + tok_region(bt.uoff[b], b);
+  uint8_t *lens = L.lens();
   int pos = skip;
   int out = 0, ntok = 0;
   bool ok = true;
+#ifdef SBAM_WAVE_STATS
+  uint64_t ws_[16] = {0};
+  uint64_t wt_ = __builtin_amdgcn_s_memtime();
+  const uint64_t wt0_ = wt_;
+#endif
 
   for (bool fin = false; ok && !fin;) {
-    // ---- block header (wave-uniform)
+    // ---- block header
     int wq = (pos >> 7) << 7;
     wave_stage(L.win, base, base_dw, wq >> 5, lim_dw);
+    WMARK(12);
+    if (pos + 3 > pend) { ok = false; break; }
     HBits h;
     h.init(L.win, wq, pos);
-    if (pos + 3 > pend) { ok = false; break; }
     fin = h.get(L.win, 1) != 0;
     const uint32_t type = h.get(L.win, 2);
     int hlit = 288, hdist = 32;
     if (type == 1) {  // fixed codes: lit 0-143:8, 144-255:9, 256-279:7, 280-287:8; dist 0-31:5
       for (int i = lane; i < 320; i += 64)
-        L.lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : i < 288 ? 8 : 5;
+        lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : i < 288 ? 8 : 5;
     } else if (type == 2) {
       hlit = (int)h.get(L.win, 5) + 257;
       hdist = (int)h.get(L.win, 5) + 1;
@@ -994,10 +1027,11 @@ __global__ __launch_bounds__(64) void k_inflate_wave(const uint8_t *__restrict__
       uint64_t clp = 0;
       for (int i = 0; i < 19; i++)
         if (i < hclen) clp |= (uint64_t)h.get(L.win, 3) << (3 * kClOrder[i]);
-      // code-length code: complete, 7-bit lookup table
+      // code-length code (must be complete): left-justified 7-bit limits and the symbols in canonical order
       int left = 1;
-      uint32_t first[8], code = 0;
       bool over = false;
+      uint32_t lim7[8], base7[8], code = 0;
+      int acc = 0;
 #pragma unroll
       for (int l = 1; l <= 7; l++) {
         uint32_t k = 0;
@@ -1005,67 +1039,100 @@ __global__ __launch_bounds__(64) void k_inflate_wave(const uint8_t *__restrict__
         for (int s2 = 0; s2 < 19; s2++) k += ((clp >> (3 * s2)) & 7) == (uint64_t)l ? 1u : 0u;
         left = 2 * left - (int)k;
         over |= left < 0;
-        first[l] = code;
+        lim7[l] = (code + k) << (7 - l);
+        base7[l] = (uint32_t)acc - code;
+        acc += (int)k;
         code = (code + k) << 1;
       }
       if (over || left != 0) { ok = false; break; }
-      if (lane < 19) {
-        const uint32_t l = (uint32_t)(clp >> (3 * lane)) & 7u;
-        if (l) {
-          uint32_t rank = 0;
-          for (int s2 = 0; s2 < lane; s2++) rank += ((clp >> (3 * s2)) & 7) == l ? 1u : 0u;
-          uint32_t fc = 0;
+      for (int i = lane; i < 320; i += 64) lens[i] = 0;
+      // every lane decodes the code-length symbol at bit b0 + lane: advance, repeat count, value kind
+      uint32_t srt[4] = {0, 0, 0, 0};  // symbols in canonical order, 5 bits each, 6 per dword
+      {
+        uint32_t rank = 0;
 #pragma unroll
-          for (int ll = 1; ll <= 7; ll++) fc = l == (uint32_t)ll ? first[ll] : fc;
-          const uint32_t r = __builtin_bitreverse32(fc + rank) >> (32 - l);
-          for (uint32_t k = r; k < 128; k += 1u << l) L.cl[k] = (uint8_t)((l << 5) | (uint32_t)lane);
+        for (int s2 = 0; s2 < 19; s2++) {
+          const uint32_t l = (uint32_t)(clp >> (3 * s2)) & 7u;
+          uint32_t r = 0;
+#pragma unroll
+          for (int t2 = 0; t2 < 19; t2++) {
+            const uint32_t lt2 = (uint32_t)(clp >> (3 * t2)) & 7u;
+            r += (lt2 != 0 && (lt2 < l || (lt2 == l && t2 < s2))) ? 1u : 0u;
+          }
+          if (l) {
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+              if (r / 6 == (uint32_t)q) srt[q] |= (uint32_t)s2 << (5 * (r % 6));
+          }
+          rank += l ? 1u : 0u;
         }
+        (void)rank;
       }
-      for (int i = lane; i < 320; i += 64) L.lens[i] = 0;
       __syncthreads();
+      WMARK(10);
       const int total = hlit + hdist;
-      int n = 0;
+      int n = 0, p = h.pos;
       uint32_t prev = 0;
       while (n < total) {
-        h.need(L.win);
-        const uint32_t e = L.cl[(uint32_t)h.bb & 127u];
-        const int l = (int)(e >> 5);
-        const uint32_t sym = e & 31u;
-        h.bb >>= l;
-        h.bc -= l;
-        h.pos += l;
-        int rep = 1;
-        uint32_t v = sym;
-        if (sym == 16) {
-          if (n == 0) { ok = false; break; }
-          rep = 3 + (int)h.get(L.win, 2);
-          v = prev;
-        } else if (sym == 17) {
-          rep = 3 + (int)h.get(L.win, 3);
-          v = 0;
-        } else if (sym == 18) {
-          rep = 11 + (int)h.get(L.win, 7);
-          v = 0;
-        }
-        if (n + rep > total || h.pos > pend) { ok = false; break; }
-        if (v)
-          for (int j = lane; j < rep; j += 64) {
-            const int idx = n + j;
-            L.lens[idx < hlit ? idx : 288 + idx - hlit] = (uint8_t)v;
+        // lane j: the symbol at p + j
+        const int q = p + lane - wq, w = q >> 5, sh = q & 31;
+        const uint64_t x64 = ((uint64_t)L.win[w] | ((uint64_t)L.win[w + 1] << 32)) >> sh;
+        const uint32_t bits = (uint32_t)x64;
+        const uint32_t rev = __builtin_bitreverse32(bits & 127u) >> 25;
+        uint32_t l = 1;
+#pragma unroll
+        for (int ll = 1; ll < 7; ll++) l += rev >= lim7[ll] ? 1u : 0u;
+        uint32_t bsel = 0;
+#pragma unroll
+        for (int ll = 1; ll <= 7; ll++) bsel = l == (uint32_t)ll ? base7[ll] : bsel;
+        const uint32_t idx = (rev >> (7 - l)) + bsel;
+        const uint32_t dq = idx / 6, dr = idx % 6;
+        const uint32_t sw = dq == 0 ? srt[0] : dq == 1 ? srt[1] : dq == 2 ? srt[2] : srt[3];
+        const uint32_t sym = (sw >> (5 * dr)) & 31u;
+        const uint32_t xb = sym == 16 ? 2u : sym == 17 ? 3u : sym == 18 ? 7u : 0u;
+        const uint32_t xv = (bits >> l) & ((1u << xb) - 1u);
+        const uint32_t rep = sym < 16 ? 1u : sym == 18 ? 11u + xv : 3u + xv;
+        // packed: advance (5 bits) | repeat (8) | value (4) | value is "previous" (1)
+        const uint32_t info = (l + xb) | (rep << 5) | ((sym < 16 ? sym : 0u) << 13) | ((sym == 16 ? 1u : 0u) << 17);
+        // follow the true chain through the 64 decoded offsets
+        int o = 0;  // wave-uniform (readlane from an SGPR index, no LDS round trip per step)
+        bool bad = false;
+        while (o < 64 && n < total) {
+          const uint32_t in = (uint32_t)__builtin_amdgcn_readlane((int)info, o);
+          const int adv = (int)(in & 31u), r = (int)((in >> 5) & 255u);
+          const bool isprev = (in >> 17) & 1u;
+          const uint32_t v = isprev ? prev : (in >> 13) & 15u;
+          if ((isprev && n == 0) || n + r > total) { bad = true; break; }
+          if (v) {
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+              const int j = lane + 64 * k, idx2 = n + j;
+              if (j < r) lens[idx2 < hlit ? idx2 : 288 + idx2 - hlit] = (uint8_t)v;
+            }
           }
-        n += rep;
-        prev = v;
+          n += r;
+          prev = v;
+          o = __builtin_amdgcn_readfirstlane(o + adv);
+        }
+        if (bad) { ok = false; break; }
+        p += o;
+        if (p > pend) { ok = false; break; }
       }
       if (!ok) break;
+      WMARK(11);
+      h.pos = p;
       __syncthreads();
-      if (L.lens[256] == 0) { ok = false; break; }  // no end-of-block code
+      if (lens[256] == 0) { ok = false; break; }  // no end-of-block code
     } else {  // stored (rare in BGZF) or invalid: the slow decoder
       ok = false;
       break;
     }
     if (h.pos > pend) { ok = false; break; }
-    if (!wave_build<true>(L, 288, hdist, L.dist, kDistCap)) { ok = false; break; }
-    if (!wave_build<false>(L, 0, hlit, L.lit, kLitCap)) { ok = false; break; }
+    WMARK(0);
+    WADD(9, 1);
+    if (!wave_build<true>(L, 288, hdist, kDistOff, kDistSub)) { ok = false; break; }
+    if (!wave_build<false>(L, 0, hlit, kLitOff, kLitSub)) { ok = false; break; }
+    WMARK(1);
 
     // ---- data rounds: 64 segments of kK bits per round
     uint32_t S = (uint32_t)h.pos << 10;  // round start: pos << 10 | state << 9 | pending match length
@@ -1073,167 +1140,199 @@ __global__ __launch_bounds__(64) void k_inflate_wave(const uint8_t *__restrict__
       const int Sp = (int)(S >> 10);
       wq = (Sp >> 7) << 7;
       wave_stage(L.win, base, base_dw, wq >> 5, lim_dw);
+      WMARK(2);
+      WADD(6, 1);
       const int seg_start = lane == 0 ? Sp : Sp + lane * kK;
       const int seg_end = Sp + (lane + 1) * kK;
-      // phase A: every lane decodes its segment from a guessed start (lane 0: the true one)
-      uint32_t bA[kM], cA[kM];
-      uint32_t tokA = 0, bytA = 0, exitA;
-      int stopA = ST_NONE;
+      // ---- phase A: every lane decodes its segment from a guessed start (lane 0: the true one)
+      uint32_t cp[kCp], cc[kCp];  // checkpoints: position (literal/length state) and tok | byt << 12 there
+      sfor<0, kCp>([&](auto I) {
+        cp[decltype(I)::value] = ~0u;
+        cc[decltype(I)::value] = 0;
+      });
+      uint32_t s1p = ~0u, s1e = 0, s1c = 0, s2p = ~0u, s2e = 0, s2c = 0;  // stops: start, exit | kind, counts
+      int nst = 0;
+      uint32_t tokA = 0, bytA = 0, exitEnd;
       {
         int stt = lane == 0 ? (int)((S >> 9) & 1) : 0;
         uint32_t pl = lane == 0 ? (S & 511u) : 0u;
-        WBits r;
-        bool done = false;
+        int rp = seg_start;  // reader position
+        bool go = true;
         if (seg_start >= pend && lane > 0) {
-          stopA = ST_OUT;
-          done = true;
-          r.pos = seg_start;
-        } else {
-          wb_init(r, L.win, wq, seg_start);
+          go = false;
+          nst = 1;
+          s1p = (uint32_t)seg_start;
+          s1e = ((uint32_t)seg_start << 10) | (uint32_t)ST_OUT;
         }
         auto step = [&]() {
+          const uint32_t p0 = (uint32_t)rp;
           uint32_t v;
-          const uint32_t e = wb_symbol(r, L, stt, v);
-          const uint32_t kind = (e >> 8) & 3;
-          if (r.pos > pend) stopA = ST_OUT;
-          else if (kind == K_SPEC) stopA = v == 0 ? ST_EOB : ST_ERR;
-          else {
-            tokA++;
-            bytA += kind == K_LIT ? 1u : kind == K_LEN ? v : 0u;
-            pl = kind == K_LEN ? v : pl;
-            stt = kind == K_LEN ? 1 : 0;
+          const uint32_t kind = (wsym(L, wq, rp, stt, v) >> 8) & 3u;
+          const bool outp = rp > pend;
+          const bool stp = kind == K_SPEC || outp;
+          if (stp) {  // rare: record the stop (exit in the literal state | kind) and decode on
+            const uint32_t ek = ((uint32_t)rp << 10) | (uint32_t)(outp ? ST_OUT : v == 0 ? ST_EOB : ST_ERR);
+            const uint32_t cn = tokA | (bytA << 12);
+            const bool w1 = nst == 0, w2 = nst == 1;
+            s1p = w1 ? p0 : s1p;
+            s1e = w1 ? ek : s1e;
+            s1c = w1 ? cn : s1c;
+            s2p = w2 ? p0 : s2p;
+            s2e = w2 ? ek : s2e;
+            s2c = w2 ? cn : s2c;
+            nst++;
+            go = !outp;
           }
-          done = stopA != ST_NONE;
+          tokA += stp ? 0u : 1u;
+          bytA += stp ? 0u : kind == K_LIT ? 1u : kind == K_LEN ? v : 0u;
+          pl = (!stp && kind == K_LEN) ? v : pl;
+          stt = (!stp && kind == K_LEN) ? 1 : 0;
         };
-        sfor<0, kM>([&](auto I) {
-          constexpr int k = decltype(I)::value;
-          bA[k] = ~0u;
-          cA[k] = 0;
-          if (!done && r.pos < seg_end) {
-            bA[k] = stt == 0 ? (uint32_t)r.pos : ~0u;
-            cA[k] = tokA | (bytA << 12);
-            step();
-          }
+        // checkpoints every kCpSteps steps (wave-uniform, so a record costs no divergent branch): the lane's
+        // position if it is at a literal/length boundary
+        sfor<0, kCp>([&](auto J) {
+          constexpr int jj = decltype(J)::value;
+          const bool live = go && rp < seg_end;
+          cp[jj] = (live && stt == 0) ? (uint32_t)rp : ~0u;
+          cc[jj] = tokA | (bytA << 12);
+#pragma unroll 1
+          for (int k = 0; k < kCpSteps; k++)
+            if (go && rp < seg_end) step();
         });
-        while (!done && r.pos < seg_end) step();
-        exitA = ((uint32_t)r.pos << 10) | ((uint32_t)stt << 9) | pl;
+        while (go && rp < seg_end) step();
+        exitEnd = ((uint32_t)rp << 10) | ((uint32_t)stt << 9) | pl;
       }
-      // phase B: lanes whose true start differs re-decode until they meet their own first-pass path
-      uint32_t exitk = exitA, tok = tokA, byt = bytA;
-      int stop = stopA;
+      WMARK(3);
+      // the lane's result if its guessed start is the true one: the path ends at its first stop
+      const SegResult own = nst > 0 ? SegResult{s1c & 4095u, s1c >> 12, s1e & ~1023u, (int)(s1e & 3u), false}
+                                    : SegResult{tokA, bytA, exitEnd, ST_NONE, false};
+      // ---- phase B: lanes whose true start differs re-decode it until they reach a first-pass checkpoint
+      SegResult res = own;
+      uint32_t nxt = lane == 0 ? own.exit : exitEnd;  // what the right neighbour starts from (provisional)
       uint32_t bst = lane == 0 ? S : ((uint32_t)seg_start << 10);
+      bool ver = lane == 0;
       int f = 64;
       for (;;) {
-        uint32_t pex = __shfl_up(exitk, 1);
+        uint32_t pex = __shfl_up(nxt, 1);
         if (lane == 0) pex = S;
-        const uint64_t stops = __ballot(stop != ST_NONE);
-        f = stops ? __ffsll((unsigned long long)stops) - 1 : 64;
+        bool upd = false;
+        if (!ver && pex == bst) {  // the guessed start was right
+          ver = true;
+          upd = nxt != own.exit;
+          nxt = own.exit;
+          res = own;
+        }
+        const uint64_t vs = __ballot(ver && res.stop != ST_NONE);
+        f = uni(vs ? __ffsll((unsigned long long)vs) - 1 : 64);
         const bool need = lane > 0 && lane <= f && pex != bst;
-        if (__ballot(need) == 0) break;
+        if (__ballot(need || upd) == 0) break;
+        WADD(7, 1);
         if (need) {
           int stt = (int)((pex >> 9) & 1);
           uint32_t pl = pex & 511u, tk = 0, by = 0;
-          WBits r;
-          wb_init(r, L.win, wq, (int)(pex >> 10));
-          int sp = ST_NONE;
+          int rp = (int)(pex >> 10);
+          // the first checkpoint at or after the reader
+          auto next_cp = [&](uint32_t p) {
+            uint32_t m = ~0u;
+            sfor<0, kCp>([&](auto I) {
+              const uint32_t x = cp[decltype(I)::value];
+              m = (x >= p && x < m) ? x : m;
+            });
+            return m;
+          };
+          uint32_t tcp = next_cp((uint32_t)rp);
           for (;;) {
-            if (stt == 0) {
-              int hit = -1;
+            if (stt == 0 && (uint32_t)rp == tcp) {  // on the first-pass path from here
               uint32_t cj = 0;
-              sfor<0, kM>([&](auto I) {
-                constexpr int k = decltype(I)::value;
-                if (bA[k] == (uint32_t)r.pos) {
-                  hit = k;
-                  cj = cA[k];
-                }
-              });
-              if (hit >= 0) {  // on the first-pass path from here: its exit, stop and remaining counts hold
-                tok = tk + tokA - (cj & 4095u);
-                byt = by + bytA - (cj >> 12);
-                stop = stopA;
-                exitk = exitA;
+              sfor<0, kCp>([&](auto I) { cj = cp[decltype(I)::value] == tcp ? cc[decltype(I)::value] : cj; });
+              const uint32_t P = tcp;
+              // the first recorded stop at or after the checkpoint ends the path
+              const bool h1 = nst >= 1 && s1p >= P, h2 = !h1 && nst >= 2 && s2p >= P;
+              if (h1 || h2) {
+                const uint32_t se = h1 ? s1e : s2e, sc = h1 ? s1c : s2c;
+                res = SegResult{tk + (sc & 4095u) - (cj & 4095u), by + (sc >> 12) - (cj >> 12), se & ~1023u,
+                                (int)(se & 3u), false};
                 break;
               }
+              if (nst <= 2) {
+                res = SegResult{tk + tokA - (cj & 4095u), by + bytA - (cj >> 12), exitEnd, ST_NONE, false};
+                break;
+              }
+              tcp = ~0u;  // more stops than recorded, the first after P unknown: decode the rest here
             }
-            if (r.pos >= seg_end) {
-              tok = tk;
-              byt = by;
-              stop = ST_NONE;
-              exitk = ((uint32_t)r.pos << 10) | ((uint32_t)stt << 9) | pl;
+            if (rp >= seg_end) {
+              res = SegResult{tk, by, ((uint32_t)rp << 10) | ((uint32_t)stt << 9) | pl, ST_NONE, false};
               break;
             }
             uint32_t v;
-            const uint32_t e = wb_symbol(r, L, stt, v);
-            const uint32_t kind = (e >> 8) & 3;
-            if (r.pos > pend) sp = ST_OUT;
-            else if (kind == K_SPEC) sp = v == 0 ? ST_EOB : ST_ERR;
-            if (sp != ST_NONE) {
-              tok = tk;
-              byt = by;
-              stop = sp;
-              exitk = ((uint32_t)r.pos << 10) | ((uint32_t)stt << 9) | pl;
+            const uint32_t kind = (wsym(L, wq, rp, stt, v) >> 8) & 3u;
+            const bool outp = rp > pend;
+            if (kind == K_SPEC || outp) {
+              res = SegResult{tk, by, (uint32_t)rp << 10, outp ? ST_OUT : v == 0 ? ST_EOB : ST_ERR, false};
               break;
             }
             tk++;
             by += kind == K_LIT ? 1u : kind == K_LEN ? v : 0u;
             pl = kind == K_LEN ? v : pl;
             stt = kind == K_LEN ? 1 : 0;
+            if ((uint32_t)rp > tcp) tcp = next_cp((uint32_t)rp);
           }
+          nxt = res.stop != ST_NONE ? res.exit : res.exit;
+          ver = true;
           bst = pex;
         }
       }
+      WMARK(4);
       // lanes 0..f carry the true path (f: the lane whose segment ends the deflate block, or 64)
       const bool act = lane <= f;
-      const uint32_t my_tok = act ? tok : 0u, my_byt = act ? byt : 0u;
+      const uint32_t my_tok = act ? res.tok : 0u, my_byt = act ? res.byt : 0u;
       const uint32_t itok = wave_incl_scan(my_tok), ibyt = wave_incl_scan(my_byt);
-      const uint32_t tot_tok = __shfl(itok, 63), tot_byt = __shfl(ibyt, 63);
-      const int stop_f = f < 64 ? __shfl(stop, f) : ST_NONE;
-      if (stop_f == ST_ERR || stop_f == ST_OUT || out + (int)tot_byt > us) { ok = false; break; }
-      // phase C: decode the true segments again, writing tokens at their offsets
+      const uint32_t tot_tok = uni((uint32_t)__shfl(itok, 63)), tot_byt = uni((uint32_t)__shfl(ibyt, 63));
+      const int stop_f = f < 64 ? uni(__shfl(res.stop, f)) : ST_NONE;
+      if (stop_f == ST_ERR || stop_f == ST_OUT || out + (int)tot_byt > us || __ballot(act && res.bad) != 0) {
+        ok = false;
+        break;
+      }
+      // ---- phase C: decode the true segments again, writing tokens at their offsets
       bool derr = false;
       if (act) {
-        uint32_t start = __shfl_up(exitk, 1);
+        uint32_t start = __shfl_up(nxt, 1);
         if (lane == 0) start = S;
         int stt = (int)((start >> 9) & 1);
         uint32_t pl = start & 511u;
-        WBits r;
-        wb_init(r, L.win, wq, (int)(start >> 10));
+        int rp = (int)(start >> 10);
         int o = out + (int)(ibyt - my_byt);
-        uint32_t ti = (uint32_t)ntok + (itok - my_tok), hold = 0;
-        bool has = false;
-        while (r.pos < seg_end) {
+        uint32_t ti = (uint32_t)ntok + (itok - my_tok);
+        while (rp < seg_end) {
           uint32_t v;
-          const uint32_t e = wb_symbol(r, L, stt, v);
-          const uint32_t kind = (e >> 8) & 3;
+          const uint32_t kind = (wsym(L, wq, rp, stt, v) >> 8) & 3u;
           if (kind == K_SPEC) break;  // the end-of-block symbol of lane f
           const uint32_t t = kind == K_LIT ? v : kind == K_LEN ? v + 253u : v - 1u;
           if (kind == K_DIST) derr |= (int)v > o - (int)pl;
           o += kind == K_LIT ? 1 : kind == K_LEN ? (int)v : 0;
           pl = kind == K_LEN ? v : pl;
           stt = kind == K_LEN ? 1 : 0;
-          if (ti & 1u) {
-            if (has) *reinterpret_cast<uint32_t *>(reg + 2 * (ti - 1)) = hold | (t << 16);
-            else *reinterpret_cast<uint16_t *>(reg + 2 * ti) = (uint16_t)t;
-            has = false;
-          } else {
-            hold = t;
-            has = true;
-          }
+          *reinterpret_cast<uint16_t *>(reg + 2 * ti) = (uint16_t)t;
           ti++;
         }
-        if (has) *reinterpret_cast<uint16_t *>(reg + 2 * (ti - 1)) = (uint16_t)hold;
       }
+      WMARK(5);
       if (__ballot(derr) != 0) { ok = false; break; }
       out += (int)tot_byt;
       ntok += (int)tot_tok;
       if (f < 64) {  // end of block: the next header follows lane f's end-of-block symbol
-        pos = (int)(__shfl(exitk, f) >> 10);
+        pos = (int)(uni((uint32_t)__shfl(res.exit, f)) >> 10);
         break;
       }
-      S = __shfl(exitk, 63);
+      S = uni((uint32_t)__shfl(nxt, 63));
     }
   }
   if (ok && out != us) ok = false;
+#ifdef SBAM_WAVE_STATS
+  ws_[8] = __builtin_amdgcn_s_memtime() - wt0_;
+  if (lane == 0)
+    for (int i = 0; i < 16; i++) atomicAdd(&g_wave_stats[i], (unsigned long long)ws_[i]);
+#endif
   if (lane == 0) {
     if (ok) {
       status[b] = INF_OK;

@@ -123,11 +123,15 @@ def test_inflate_corrupted_payloads(seed):
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(4))
 def test_wave_decoder_takes_every_compressed_block(seed):
-    """Only the stored (level 0) blocks go to the per-lane fallback; fixed, dynamic, Huffman-only and RLE blocks
-    are decoded by the wave-parallel decoder (whose output test_inflate_shapes_bit_exact checks)."""
+    """Only the payloads of stored DEFLATE blocks (level 0, and incompressible data at any level) go to the
+    per-lane fallback; fixed, dynamic, Huffman-only and RLE blocks are decoded by the wave-parallel decoder (whose
+    output test_inflate_shapes_bit_exact checks)."""
     import sbam
     data = build_file(seed)
-    stored = sum(1 for i in range(len(sample_inputs(seed))) if SHAPES[(i + seed) % len(SHAPES)][0] == 0)
+    stored = 0
+    for i, raw in enumerate(sample_inputs(seed)):
+        level, strat = SHAPES[(i + seed) % len(SHAPES)]
+        stored += ((deflate(raw, level, strat)[0] >> 1) & 3) == 0  # first block's BTYPE
     g = sbam.BamFile(data, inflate=False)
     try:
         g.inflate()

@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Diagnostic (tools-only build, `make -C spark-bam_amd EXTRA=-DSBAM_WAVE_STATS BUILD=build_stats`): cycle
+attribution inside k_inflate_wave (s_memtime per phase, summed over waves) on a synthetic BAM."""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("SBAM_LIB", os.path.join(ROOT, "spark-bam_amd", "build_stats", "libsbam.so"))
+sys.path[:0] = [os.path.join(ROOT, "spark-bam_amd"), os.path.join(ROOT, "tools")]
+import numpy as np  # noqa: E402
+import sbam  # noqa: E402
+import synth  # noqa: E402
+
+size = float(sys.argv[1]) if len(sys.argv) > 1 else 1.0
+s = synth.SynthBam.for_size(int(size * 1e9), tile_mb=min(64.0, size * 300))
+f = sbam.BamFile(s.bytes(), inflate=False)
+L = sbam.load_library()
+fn = L.sbam_debug_wave_stats
+fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+buf = (ctypes.c_ulonglong * 16)()
+f.reset(); f.run(contig_lengths=s.contig_lengths)
+fn(buf, 1)
+f.reset(); f.run(contig_lengths=s.contig_lengths)
+fn(buf, 1)
+v = list(buf)
+names = ["header", "build", "stage", "phaseA", "phaseB", "scanC", "rounds", "b_iters", "total", "headers",
+         "hdr_cl_setup", "hdr_chain", "hdr_stage"]
+tot = v[8]
+out = {n: v[i] for i, n in enumerate(names)}
+out.update({f"{n}_pct": round(100.0 * v[i] / tot, 1) for i, n in enumerate(names[:6])})
+out["blocks"] = int(f.n_blocks)
+out["decode_ms"] = f.kernel_ms("inflate_decode")
+out["fallbacks"] = f.inflate_fallbacks()
+out["b_iters_per_round"] = round(v[7] / max(v[6], 1), 3)
+out["rounds_per_block"] = round(v[6] / out["blocks"], 3)
+out["cycles_per_header"] = {n: round(v[i] / max(v[9], 1)) for i, n in ((0, "rest"), (10, "cl_setup"), (11, "chain"), (12, "stage"), (1, "build"))}
+out["cycles_per_round"] = {n: round(v[i] / max(v[6], 1)) for i, n in enumerate(names[2:6], 2)}
+print(json.dumps(out))
