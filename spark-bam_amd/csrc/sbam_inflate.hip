@@ -1094,26 +1094,42 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         const uint32_t rep = sym < 16 ? 1u : sym == 18 ? 11u + xv : 3u + xv;
         // packed: advance (5 bits) | repeat (8) | value (4) | value is "previous" (1)
         const uint32_t info = (l + xb) | (rep << 5) | ((sym < 16 ? sym : 0u) << 13) | ((sym == 16 ? 1u : 0u) << 17);
-        // follow the true chain through the 64 decoded offsets
-        int o = 0;  // wave-uniform (readlane from an SGPR index, no LDS round trip per step)
-        bool bad = false;
+        // the true chain through the 64 decoded offsets: only the offsets and the running count are serial
+        // (scalar: one readlane per symbol); values, repeat targets and LDS writes follow for all members at once
+        int o = 0;
+        uint64_t chain = 0;
+        const int n0 = n;
         while (o < 64 && n < total) {
           const uint32_t in = (uint32_t)__builtin_amdgcn_readlane((int)info, o);
-          const int adv = (int)(in & 31u), r = (int)((in >> 5) & 255u);
-          const bool isprev = (in >> 17) & 1u;
-          const uint32_t v = isprev ? prev : (in >> 13) & 15u;
-          if ((isprev && n == 0) || n + r > total) { bad = true; break; }
-          if (v) {
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-              const int j = lane + 64 * k, idx2 = n + j;
-              if (j < r) lens[idx2 < hlit ? idx2 : 288 + idx2 - hlit] = (uint8_t)v;
-            }
-          }
-          n += r;
-          prev = v;
-          o = __builtin_amdgcn_readfirstlane(o + adv);
+          chain |= 1ull << o;
+          n += (int)((in >> 5) & 255u);
+          o += (int)(in & 31u);
         }
+        o = uni(o);
+        n = uni(n);
+        const bool mem = (chain >> lane) & 1ull;
+        const uint64_t below = (1ull << lane) - 1ull;
+        // each member's first code-length index: n0 + the repeats of the members before it
+        const uint32_t rr = mem ? (info >> 5) & 255u : 0u;
+        const int nst0 = n0 + (int)(wave_incl_scan(rr) - rr);
+        // value: a literal length, 0 for 17/18, and for 16 the value of the nearest member before it that has one
+        // (the previous batch's last value when there is none)
+        const bool isprev = (info >> 17) & 1u;
+        const uint32_t own_v = (info >> 13) & 15u;
+        const uint64_t hv = __ballot(mem && !isprev);
+        const uint64_t hb = hv & below;
+        const int src = hb ? 63 - __clzll((long long)hb) : 0;
+        const uint32_t pv = (uint32_t)__shfl((int)own_v, src);
+        const uint32_t v = isprev ? (hb ? pv : prev) : own_v;
+        bool bad = n > total || __ballot(mem && isprev && nst0 == 0) != 0;
+        if (mem && v) {
+          for (int k = 0; k < (int)rr; k++) {  // <= 6 (a literal: 1; code 16: 3-6; zeros need no write)
+            const int idx2 = nst0 + k;
+            lens[idx2 < hlit ? idx2 : 288 + idx2 - hlit] = (uint8_t)v;
+          }
+        }
+        const int last = chain ? 63 - __clzll((long long)chain) : 0;
+        prev = uni((uint32_t)__shfl((int)v, last));
         if (bad) { ok = false; break; }
         p += o;
         if (p > pend) { ok = false; break; }
