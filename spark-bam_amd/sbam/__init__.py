@@ -43,6 +43,18 @@ WORD_HALO = 0x00800000
 BGZF_BLOCKS_TO_CHECK = 5
 READS_TO_CHECK = 10
 MAX_READ_SIZE = 10_000_000
+# Hadoop's local FileSystem block size (fs.local.block.size default): what a split size falls back to when
+# -m/--max-split-size is unset (check/.../args/SplitSize.scala:10-17: "default to underlying FileSystem's value").
+LOCAL_FS_BLOCK_SIZE = 32 << 20
+
+
+def effective_split_size(max_split_size: Optional[int] = None, fs_block_size: int = LOCAL_FS_BLOCK_SIZE) -> int:
+    """The split size Hadoop's FileInputFormat uses: computeSplitSize(blockSize, minSize=1, maxSize) =
+    max(1, min(maxSize, blockSize)), with maxSize = the FS block size when -m is unset (SplitSize.scala:10-17).
+    The FS-block cap comes from Hadoop, outside the reference tree: parity unpinned (no golden splits a file into
+    pieces larger than 32 MiB)."""
+    m = fs_block_size if max_split_size is None else int(max_split_size)
+    return max(1, min(m, fs_block_size))
 
 
 class SbamError(Exception):

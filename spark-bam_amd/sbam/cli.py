@@ -516,7 +516,9 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                  "index-records"):
         p = sub.add_parser(name)
         p.add_argument("-l", "--print-limit", type=int, default=10)
-        p.add_argument("-m", "--max-split-size", type=parse_bytes, default=2 << 20)
+        # check-blocks defaults to 2 MB (blocks/CheckBlocks.scala via Blocks.scala:64); compute-splits and
+        # count-reads to the FileSystem's split size (args/SplitSize.scala:10-17)
+        p.add_argument("-m", "--max-split-size", type=parse_bytes, default=(2 << 20) if name == "check-blocks" else None)
         p.add_argument("bam")
         p.add_argument("out", nargs="?")
         if name in ("full-check", "check-bam"):
@@ -547,9 +549,9 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
         elif a.cmd == "index-records":
             lines = index_records_lines(f)
         elif a.cmd == "compute-splits":
-            lines = compute_splits_lines(f, a.max_split_size, a.print_limit)
+            lines = compute_splits_lines(f, sbam.effective_split_size(a.max_split_size), a.print_limit)
         else:
-            lines = count_reads_lines(f, a.max_split_size)
+            lines = count_reads_lines(f, sbam.effective_split_size(a.max_split_size))
     text = "\n".join(lines) + "\n"
     if a.out:
         open(a.out, "w").write(text)

@@ -164,3 +164,33 @@ def test_count_reads_report(tmp_path):
     lines = out.read_text().split("\n")
     assert re.fullmatch(r"spark-bam read-count time: \d+", lines[0])
     assert lines[2] == "spark-bam found 4917 reads"
+
+
+def test_split_size_defaults_follow_hadoop():
+    """-m unset: compute-splits / count-reads use the FileSystem's split size (SplitSize.scala:10-17; the local FS
+    block is 32 MiB), check-blocks 2 MB; a larger -m is capped at the FS block (FileInputFormat.computeSplitSize).
+    The cap and the local default come from Hadoop, outside the reference tree: parity unpinned."""
+    import sbam
+    from sbam import cli
+    assert sbam.effective_split_size(None) == 32 << 20
+    assert sbam.effective_split_size(2 << 20) == 2 << 20
+    assert sbam.effective_split_size(64 << 20) == 32 << 20
+    assert sbam.effective_split_size(64 << 20, fs_block_size=128 << 20) == 64 << 20
+    import argparse
+    seen = {}
+    orig = argparse.ArgumentParser.parse_args
+
+    def capture(self, argv=None, ns=None):
+        a = orig(self, argv, ns)
+        seen[a.cmd] = a.max_split_size
+        raise SystemExit(0)
+    argparse.ArgumentParser.parse_args = capture
+    try:
+        for cmd in ("compute-splits", "count-reads", "check-blocks"):
+            try:
+                cli.main([cmd, "x.bam"])
+            except SystemExit:
+                pass
+    finally:
+        argparse.ArgumentParser.parse_args = orig
+    assert seen == {"compute-splits": None, "count-reads": None, "check-blocks": 2 << 20}
