@@ -134,53 +134,6 @@ def cpu_baseline(sample_mb: float, threads: int, split_size: int, seed: int):
                       f"compute-splits @ {split_size >> 20} MiB, {wall:.2f} s wall"}
 
 
-class WindowPipe:
-    """A rank's byte range streamed through two contexts in W windows: while window w computes on one context, a
-    loader thread makes window w+1's bytes resident in the other (host staging by `stage`, then sbam_load's
-    pinned host → device copy).  A step starts with window 0 loaded in the foreground, so every step is a
-    complete host → results pass."""
-
-    def __init__(self, wplans, stage, split_size, contig_lengths, device, run_window):
-        from concurrent.futures import ThreadPoolExecutor
-        from sbam import dist as sdist
-        self.sdist = sdist
-        self.wplans, self.stage, self.split_size = wplans, stage, split_size
-        self.contig_lengths, self.device, self.run_window = contig_lengths, device, run_window
-        self.loader = ThreadPoolExecutor(max_workers=1)
-        self.ctx = [None, None]
-
-    def _load(self, w, j):
-        wp = self.wplans[w]
-        sh = self.ctx[j]
-        lo, hi = wp.load_range(sh.halo if sh is not None else 2 << 20)
-        buf = self.stage(lo, hi, j)
-        if sh is None:
-            self.ctx[j] = self.sdist.GpuShard(wp, lambda a, b: buf if (a, b) == (lo, hi) else self.stage(a, b, j),
-                                              self.split_size, self.contig_lengths, device=self.device)
-        else:
-            sh.reload(wp, buf)
-        return self.ctx[j]
-
-    def step(self):
-        W = len(self.wplans)
-        out = []
-        fut = None
-        sh = self._load(0, 0)
-        for w in range(W):
-            if w > 0:
-                sh = fut.result()
-            if w + 1 < W:
-                fut = self.loader.submit(self._load, w + 1, (w + 1) % 2)
-            out.append(self.run_window(sh))
-        return out
-
-    def close(self):
-        self.loader.shutdown()
-        for sh in self.ctx:
-            if sh is not None:
-                sh.close()
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -296,7 +249,7 @@ def main():
                 fu.result()
             return buf
 
-        pipe = WindowPipe(wplans_of(W), stage_synth, split_size, s.contig_lengths, local, run_window)
+        pipe = sdist.WindowPipe(wplans_of(W), stage_synth, split_size, s.contig_lengths, local, run_window)
 
     def step():
         res, ms = merge([run_window(shard)] if W == 1 else pipe.step())
@@ -384,7 +337,7 @@ def main():
         def stage_pinned(lo, hi, j):
             return hv[lo - lo0:hi - lo0] if lo >= lo0 and hi <= hi0 else s.slice(lo, hi)
 
-        epipe = WindowPipe(wplans_of(args.e2e_windows), stage_pinned, split_size, s.contig_lengths, local,
+        epipe = sdist.WindowPipe(wplans_of(args.e2e_windows), stage_pinned, split_size, s.contig_lengths, local,
                            run_window)
         merge(epipe.step())  # warm-up (allocations)
         sync()

@@ -13,11 +13,18 @@ r+1 starts.  The only cross-GPU traffic is what Spark's driver does with tiny da
 A chain that leaves the loaded bytes reports HALO; the shard doubles its halo and re-runs (adaptive halo
 for long reads).  ``compute`` is pluggable so the distributed logic is testable on CPU (gloo) with a
 CPU-side per-shard function; production uses ``GpuShard``.
+
+``run_file`` is the file-level driver: rank 0 parses the BAM header and broadcasts ContigLengths
+(CanLoadBam.scala:179-180: the driver reads the header once and ships it to every task), every rank preads
+only its own byte range + halo, and without a process group the same shards run one after another on this
+process's GPU (a file larger than one GPU's HBM, or a one-GPU rehearsal of an N-GPU run).  ``WindowPipe`` streams
+one rank's range through two contexts in windows (CanLoadBam.scala:281-334 at more than HBM per GPU).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
-from typing import Callable, List, Optional, Sequence
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -172,6 +179,18 @@ class GpuShard:
             return shard_load(self.f, self.plan, self.split_size, self.R)
         return self._retry(once)
 
+    def load_columns(self, columns: Sequence[str]):
+        """load_step with the decoded record columns copied out: (partition sizes, {column: ndarray})."""
+        def once():
+            self.f.reset()
+            self.f.run(contig_lengths=self.contig_lengths)
+            p = self.plan
+            if not p.split_count:
+                return np.zeros(0, np.int64), {k: np.zeros(0, self.sbam.RECORD_COLUMNS[k]) for k in columns}
+            return self.f.load_records(self.split_size, first=p.split_first, count=p.split_count,
+                                       reads_to_check=self.R, columns=columns)
+        return self._retry(once)
+
     def close(self):
         if self.f is not None:
             self.f.close()
@@ -219,3 +238,170 @@ def gather_results(res: ShardResult, plans: Sequence[ShardPlan], device=None) ->
         results.append(ShardResult(merged if r == 0 else np.zeros_like(merged), out[r, 0, :n], out[r, 1, :n],
                                    out[r, 2, :n], out[r, 3, :n]))
     return results
+
+
+# ---- file-level driver ----------------------------------------------------------------------------------------
+
+def file_source(path: str) -> Tuple[Callable[..., np.ndarray], int]:
+    """(source, file size) for a BAM on disk: source(lo, hi[, out]) preads bytes [lo, hi) into a new (or the given)
+    uint8 array — a rank touches only its own byte range, never the whole file."""
+    size = os.path.getsize(path)
+
+    def source(lo: int, hi: int, out: Optional[np.ndarray] = None) -> np.ndarray:
+        hi = min(hi, size)
+        buf = np.empty(hi - lo, np.uint8) if out is None else out[: hi - lo]
+        mv = memoryview(buf)
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            got = 0
+            while got < hi - lo:
+                n = os.preadv(fd, [mv[got: min(hi - lo, got + (1 << 30))]], lo + got)
+                if n <= 0:
+                    raise IOError(f"{path}: short read at {lo + got}")
+                got += n
+        finally:
+            os.close(fd)
+        return buf
+
+    return source, size
+
+
+def read_contig_lengths(source: Callable[[int, int], np.ndarray], file_size: int, device: int = 0,
+                        probe: int = 1 << 20) -> np.ndarray:
+    """ContigLengths from the header at the start of the file (ContigLengths.scala:20-37 via htsjdk's header
+    reader): the first `probe` bytes are inflated on the GPU and parsed (sbam_header); a header longer than the
+    probe doubles it."""
+    import sbam
+    hi = min(file_size, probe)
+    while True:
+        try:
+            with sbam.BamFile(source(0, hi), device=device, file_size=file_size, inflate=False) as f:
+                f.inflate()
+                return f.header()[1]
+        except sbam.SbamError as e:
+            if "truncated header" not in str(e) or hi >= file_size:
+                raise
+            hi = min(file_size, 2 * hi)
+
+
+def broadcast_lengths(lens: Optional[np.ndarray], device=None) -> np.ndarray:
+    """Rank 0's ContigLengths to every rank (the reference broadcasts the header's lengths to its tasks)."""
+    import torch
+    import torch.distributed as dist
+    n = torch.tensor([0 if lens is None else len(lens)], dtype=torch.int64, device=device)
+    dist.broadcast(n, src=0)
+    t = torch.zeros(int(n.item()), dtype=torch.int64, device=device)
+    if dist.get_rank() == 0:
+        t.copy_(torch.from_numpy(np.asarray(lens, np.int64)))
+    dist.broadcast(t, src=0)
+    return t.cpu().numpy()
+
+
+@dataclass
+class RunResult:
+    splits: list  # [sbam.Split] (compute-splits)
+    partition_sizes: List[int]  # records per Hadoop split
+    counts: dict  # merged full-check Counts (unpack_counts)
+    contig_lengths: np.ndarray
+
+
+def _dist_ready() -> bool:
+    try:
+        import torch.distributed as dist
+        return dist.is_available() and dist.is_initialized()
+    except ImportError:
+        return False
+
+
+def run_file(path, split_size: Optional[int] = None, world: Optional[int] = None, device: Optional[int] = None,
+             halo: int = 2 << 20, reads_to_check: int = 10, coll_device=None,
+             open_shard: Optional[Callable[[ShardPlan, Callable, int, np.ndarray], object]] = None,
+             read_header: Optional[Callable[[Callable, int, int], np.ndarray]] = None) -> RunResult:
+    """full-check + compute-splits of one BAM over byte-range shards (FullCheck.scala:141-191 with the splits of
+    CanLoadBam.scala:245-279).  `path`: a file name, or a (source, file_size) pair.
+
+    In a torch.distributed process group (RCCL on GPUs; gloo to rehearse) the shards are the ranks: rank 0 reads
+    the header and broadcasts ContigLengths, each rank preads [lo, owned_hi + halo) of its own shard, and the
+    results meet in one all_gather + one all_reduce (gather_results); every rank returns the whole result.
+    Without a process group, `world` shards (default 1) run one after another on `device`.
+    `open_shard(plan, source, split_size, contig_lengths)` / `read_header(source, size, device)` replace the GPU
+    shard and header reader (CPU tests)."""
+    import sbam
+    split_size = sbam.effective_split_size(split_size)
+    source, size = file_source(path) if isinstance(path, (str, os.PathLike)) else path
+    if _dist_ready():
+        import torch.distributed as dist
+        world, rank = dist.get_world_size(), dist.get_rank()
+        ranks = [rank]
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", 0))
+    else:
+        world, rank = world or 1, 0
+        ranks = list(range(world))
+        device = 0 if device is None else device
+    read_header = read_header or read_contig_lengths
+    lens = read_header(source, size, device) if rank == 0 else None
+    if len(ranks) == 1 and world > 1:
+        lens = broadcast_lengths(lens, coll_device)
+    if open_shard is None:
+        def open_shard(plan, src, ss, cl):
+            return GpuShard(plan, src, ss, cl, device=device, halo=halo, reads_to_check=reads_to_check)
+    plans = plan_shards(size, split_size, world)
+    results = []
+    for r in ranks:
+        sh = open_shard(plans[r], source, split_size, lens)
+        try:
+            results.append(sh.step())
+        finally:
+            sh.close()
+    if len(ranks) == 1 and world > 1:
+        results = gather_results(results[0], plans, device=coll_device)
+    splits, sizes, counts = combine(results, size)
+    return RunResult(splits, sizes, unpack_counts(counts), np.asarray(lens, np.int64))
+
+
+class WindowPipe:
+    """A rank's byte range streamed through two contexts in W windows (`wplans`: the windows' ShardPlans): while
+    window w computes on one context, a loader thread makes window w+1's bytes resident in the other (host
+    staging by `stage(lo, hi, j)` into context j's buffer, then sbam_load's host → device copy).  A step starts
+    with window 0 loaded in the foreground, so every step is a complete host → results pass.  `run_window(shard)`
+    is the per-window work (GpuShard.step / load_step / anything on shard.f)."""
+
+    def __init__(self, wplans, stage, split_size, contig_lengths, device, run_window, halo: int = 2 << 20):
+        from concurrent.futures import ThreadPoolExecutor
+        self.wplans, self.stage, self.split_size = wplans, stage, split_size
+        self.contig_lengths, self.device, self.run_window, self.halo = contig_lengths, device, run_window, halo
+        self.loader = ThreadPoolExecutor(max_workers=1)
+        self.ctx = [None, None]
+
+    def _load(self, w, j):
+        wp = self.wplans[w]
+        sh = self.ctx[j]
+        lo, hi = wp.load_range(sh.halo if sh is not None else self.halo)
+        buf = self.stage(lo, hi, j)
+        if sh is None:
+            self.ctx[j] = GpuShard(wp, lambda a, b: buf if (a, b) == (lo, hi) else self.stage(a, b, j),
+                                   self.split_size, self.contig_lengths, device=self.device, halo=self.halo)
+        else:
+            sh.reload(wp, buf)
+        return self.ctx[j]
+
+    def step(self) -> list:
+        W = len(self.wplans)
+        out = []
+        fut = None
+        sh = self._load(0, 0)
+        for w in range(W):
+            if w > 0:
+                sh = fut.result()
+            if w + 1 < W:
+                fut = self.loader.submit(self._load, w + 1, (w + 1) % 2)
+            out.append(self.run_window(sh))
+        return out
+
+    def close(self):
+        self.loader.shutdown()
+        for sh in self.ctx:
+            if sh is not None:
+                sh.close()
+        self.ctx = [None, None]

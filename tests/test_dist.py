@@ -111,3 +111,134 @@ def test_plan_covers_every_split_once():
         assert plans[0].lo == 0 and plans[-1].owned_hi == 10_000_000
         for a, b in zip(plans, plans[1:]):
             assert a.owned_hi == b.lo
+
+
+class OracleShardRunner:
+    """run_file's shard interface (step/close) on the CPU oracle."""
+
+    def __init__(self, plan, source, split_size, contig_lengths):
+        import oracle
+        self.o = oracle.BamFile(source(0, plan.file_size).tobytes())
+        assert list(self.o.lens[: self.o.nref]) == list(contig_lengths)
+        self.plan, self.split_size = plan, split_size
+
+    def step(self):
+        from sbam import dist as sdist
+        return sdist.shard_pass(OracleShard(self.o, self.plan.lo), self.plan, self.split_size, 10)
+
+    def close(self):
+        pass
+
+
+def oracle_header(source, size, device):
+    import oracle
+    o = oracle.BamFile(source(0, size).tobytes())
+    return o.lens[: o.nref].copy()
+
+
+def _expected(name, split_size):
+    import oracle
+    o = oracle.BamFile(fixture_bytes(name))
+    want, parts = oracle.compute_splits(o, split_size)
+    c, npos, rbe, ns = o.counts_range(0, o.L)
+    return [f"{a}-{b}" for a, b in want], [len(p) for p in parts], c.sum(0), npos, ns
+
+
+def _run_file_worker(rank, world, port, path, split_size, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from sbam import dist as sdist
+    seen = []
+
+    def header(source, size, device):
+        seen.append(rank)
+        return oracle_header(source, size, device)
+    r = sdist.run_file(path, split_size, open_shard=OracleShardRunner, read_header=header)
+    q.put((rank, [str(s) for s in r.splits], r.partition_sizes, r.counts["totals"].tolist(),
+           r.counts["n_success"], r.contig_lengths.tolist(), seen))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name,split_size", [("2.bam", 100000), ("1.bam", 230 * 1024)])
+def test_run_file_gloo_world2(tmp_path, name, split_size):
+    """run_file over a file on disk in a world-2 gloo group: only rank 0 reads the header, the ContigLengths reach
+    rank 1 by broadcast, each rank preads its own range, and both ranks return the single-process result."""
+    import multiprocessing as mp
+    path = tmp_path / name
+    path.write_bytes(fixture_bytes(name))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_run_file_worker, args=(r, 2, port, str(path), split_size, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = sorted([q.get(timeout=120) for _ in range(2)])
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    splits, sizes, totals, npos, ns = _expected(name, split_size)
+    for rank, sp, sz, tot, nsucc, lens, seen in got:
+        assert sp == splits and sz == sizes and tot == totals.tolist() and nsucc == ns
+        assert seen == ([0] if rank == 0 else [])
+        assert lens == got[0][5]
+
+
+def test_run_file_sequential_shards(tmp_path):
+    """Without a process group, run_file runs `world` shards one after another (one GPU, or here the oracle)."""
+    from sbam import dist as sdist
+    path = tmp_path / "5k.bam"
+    path.write_bytes(fixture_bytes("5k.bam"))
+    splits, sizes, totals, npos, ns = _expected("5k.bam", 150000)
+    for world in (1, 3):
+        r = sdist.run_file(str(path), 150000, world=world, open_shard=OracleShardRunner, read_header=oracle_header)
+        assert [str(s) for s in r.splits] == splits and r.partition_sizes == sizes
+        assert np.array_equal(r.counts["totals"], totals) and r.counts["n_success"] == ns
+        assert np.array_equal(r.counts["positions"], npos)
+
+
+def test_file_source_preads_ranges(tmp_path):
+    from sbam import dist as sdist
+    data = fixture_bytes("2.bam")
+    path = tmp_path / "2.bam"
+    path.write_bytes(data)
+    src, size = sdist.file_source(str(path))
+    assert size == len(data)
+    for lo, hi in ((0, 10), (1000, 70000), (size - 5, size + 100)):
+        assert src(lo, hi).tobytes() == data[lo:min(hi, size)]
+    out = np.zeros(200, np.uint8)
+    assert src(50, 150, out).tobytes() == data[50:150]
+
+
+def _run_file_gpu_worker(rank, world, port, path, split_size, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from sbam import dist as sdist
+    r = sdist.run_file(path, split_size, device=0)
+    q.put((rank, [str(s) for s in r.splits], r.partition_sizes, r.counts["totals"].tolist(), r.counts["n_success"],
+           r.counts["positions"].tolist()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,split_size", [("2.bam", 100000), ("5k.bam", 150000)])
+def test_run_file_gloo_world2_gpu_shards(tmp_path, name, split_size):
+    """The world-2 run through GpuShard (both ranks on GPU 0, gloo collectives): pread shards, rank-0 header,
+    broadcast ContigLengths, all_gather/all_reduce — the single-process oracle result on every rank."""
+    import multiprocessing as mp
+    path = tmp_path / name
+    path.write_bytes(fixture_bytes(name))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_run_file_gpu_worker, args=(r, 2, port, str(path), split_size, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = sorted([q.get(timeout=100) for _ in range(2)])
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    splits, sizes, totals, npos, ns = _expected(name, split_size)
+    for rank, sp, sz, tot, nsucc, pos in got:
+        assert sp == splits and sz == sizes and tot == totals.tolist() and nsucc == ns and pos == npos.tolist()

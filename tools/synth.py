@@ -1,8 +1,9 @@
 """Synthetic BAM workloads for bench.py and the large-size tests (SURVEY §8(d) config specs).
 
-A synthetic file is   header blocks | tile × k | EOF marker   where a tile is a run of records cut into
-65498-byte payloads compressed at zlib level 6 (tools/synth_bam.c).  The tile ends on a record boundary, so
-the record chain runs through every seam; any byte range of the file can be produced without
+A synthetic file is   header blocks | tile × k | unplaced tail | EOF marker   where a tile is a run of records
+cut into 65498-byte payloads compressed at zlib level 6 (tools/synth_bam.c) that visits all 84 contigs, and the
+tail is the unplaced pairs (refID = pos = -1) a coordinate-sorted WGS BAM ends with (short reads only).  Tile
+and tail end on record boundaries, so the record chain runs through every seam; any byte range of the file can be produced without
 materialising the whole file (``SynthBam.slice``), which is how each rank builds its shard + halo."""
 from __future__ import annotations
 
@@ -29,6 +30,8 @@ def lib():
         L.synth_tile.restype = i64
         L.synth_tile.argtypes = [ctypes.c_uint64, i64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp),
                                  ctypes.POINTER(i64), ctypes.POINTER(i64)]
+        L.synth_unplaced.restype = i64
+        L.synth_unplaced.argtypes = L.synth_tile.argtypes
         L.synth_contigs.argtypes = [ctypes.POINTER(ctypes.c_int32), vp]
         L.synth_free.argtypes = [vp]
         L.synth_eof.restype = vp
@@ -44,7 +47,7 @@ def _take(p, n) -> np.ndarray:
 
 class SynthBam:
     def __init__(self, tile_mb: float = 64.0, copies: int = 1, read_len: int = 150, seed: int = 0x5EEDBA11,
-                 level: int = 6, threads: int = 16):
+                 level: int = 6, threads: int = 16, unplaced_mb: float | None = None):
         L = lib()
         p = ctypes.c_void_p()
         n = L.synth_header(ctypes.byref(p))
@@ -56,9 +59,17 @@ class SynthBam:
         self.eof = np.frombuffer(ctypes.string_at(L.synth_eof(), 28), np.uint8).copy()
         self.tile_records = nrec.value
         self.tile_u = ulen.value
+        if unplaced_mb is None:
+            unplaced_mb = min(1.0, tile_mb / 4) if read_len else 0.0
+        self.tail = np.zeros(0, np.uint8)
+        self.tail_records = 0
+        if unplaced_mb > 0:
+            n = L.synth_unplaced(seed, int(unplaced_mb * 3 * 2 ** 20), read_len, level, threads, ctypes.byref(p),
+                                 ctypes.byref(nrec), ctypes.byref(ulen))
+            self.tail = _take(p, n)
+            self.tail_records = nrec.value
         self.copies = copies
-        self.size = self.header.size + copies * self.tile.size + 28
-        self.n_records = copies * self.tile_records
+        self._sizes()
         nr = ctypes.c_int32(0)
         lens = np.zeros(128, np.int64)
         L.synth_contigs(ctypes.byref(nr), lens.ctypes.data)
@@ -67,10 +78,14 @@ class SynthBam:
     @staticmethod
     def for_size(target_bytes: int, tile_mb: float = 64.0, **kw) -> "SynthBam":
         s = SynthBam(tile_mb=tile_mb, copies=1, **kw)
-        s.copies = max(1, round((target_bytes - s.header.size - 28) / s.tile.size))
-        s.size = s.header.size + s.copies * s.tile.size + 28
-        s.n_records = s.copies * s.tile_records
+        s.copies = max(1, round((target_bytes - s.header.size - s.tail.size - 28) / s.tile.size))
+        s._sizes()
         return s
+
+    def _sizes(self):
+        self.body = self.header.size + self.copies * self.tile.size  # where the unplaced tail starts
+        self.size = self.body + self.tail.size + 28
+        self.n_records = self.copies * self.tile_records + self.tail_records
 
     def slice(self, lo: int, hi: int, out: np.ndarray | None = None) -> np.ndarray:
         """File bytes [lo, hi) (hi clamped to the file size)."""
@@ -82,12 +97,16 @@ class SynthBam:
             if pos < H:
                 n = min(hi, H) - pos
                 out[pos - lo: pos - lo + n] = self.header[pos: pos + n]
-            elif pos < H + self.copies * T:
+            elif pos < self.body:
                 k, o = divmod(pos - H, T)
                 n = min(hi - pos, T - o)
                 out[pos - lo: pos - lo + n] = self.tile[o: o + n]
+            elif pos < self.body + self.tail.size:
+                o = pos - self.body
+                n = min(hi - pos, self.tail.size - o)
+                out[pos - lo: pos - lo + n] = self.tail[o: o + n]
             else:
-                o = pos - H - self.copies * T
+                o = pos - self.body - self.tail.size
                 n = hi - pos
                 out[pos - lo: pos - lo + n] = self.eof[o: o + n]
             pos += n

@@ -10,7 +10,10 @@
  * lengths 10–50 kb (median 20 kb), 200–3000 CIGAR ops, names up to 63 characters, unpaired, and ~5% of
  * records larger than a 64 KiB BGZF block.
  *
- * Contig set: the 84 GRCh37 contigs of the reference's 2.bam header (ContigLengthsTest.scala:15-102).
+ * Contig set: the 84 GRCh37 contigs of the reference's 2.bam header (ContigLengthsTest.scala:15-102).  A short-read
+ * tile visits all 84 in order, an equal run of records on each (positions wrap inside the contig, so the smallest
+ * GL contigs stay in range); synth_unplaced makes the WGS tail of unplaced pairs (refID = pos = -1 for the read and
+ * its mate) that a coordinate-sorted BAM ends with.
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -94,7 +97,7 @@ static const uint8_t kQualBins[8] = {2, 6, 15, 22, 27, 33, 37, 40};
 static const uint8_t kQualCdf[8] = {2, 5, 12, 22, 35, 55, 130, 255}; /* skewed high, /255 */
 
 /* One record; read_len query bases.  ctx: running coordinate state. */
-typedef struct { int32_t ref; int32_t pos; uint64_t serial; } coord_t;
+typedef struct { int32_t ref; int32_t pos; uint64_t serial; int64_t left, per; } coord_t;
 
 static void bam_record(buf_t *b, rng_t *r, coord_t *co, int read_len, uint8_t *rec) {
   int n = 0;
@@ -107,7 +110,8 @@ static void bam_record(buf_t *b, rng_t *r, coord_t *co, int read_len, uint8_t *r
   const int lrn = (int)strlen(name) + 1;
   const int unmapped = runi(r, 1000) < 5;
   co->pos += (int32_t)runi(r, 40);
-  if (co->pos + 2000 > kLens[co->ref]) { co->ref = (co->ref + 1) % 25; co->pos = 10000; }
+  if (co->left-- <= 0) { co->ref = (co->ref + 1) % NREF; co->pos = 400; co->left = co->per - 1; }
+  if (co->pos + 2400 > kLens[co->ref]) co->pos = 400; /* mates stay inside [50, len) */
   const int32_t pos = co->pos;
   const int32_t mpos = second ? pos - 250 - (int32_t)runi(&pr, 100) : pos + 250 + (int32_t)runi(&pr, 100);
   uint32_t cig[8];
@@ -275,6 +279,39 @@ static void bam_long_record(buf_t *b, rng_t *r, coord_t *co, uint8_t *rec, uint3
   bput(b, rec, n);
   co->serial++;
 }
+/* Unplaced pair member (both reads unmapped, no coordinates): refID = pos = next refID = next pos = -1,
+ * bin 4680 (reg2bin(-1, 0)), no CIGAR, flag 77 / 141. */
+static void bam_unplaced_record(buf_t *b, rng_t *r, coord_t *co, int read_len, uint8_t *rec) {
+  int n = 0;
+  char name[64];
+  const int second = (int)(co->serial & 1);
+  rng_t pr = {(co->serial / 2) * 0x9E3779B97F4A7C15ull + 777};
+  snprintf(name, sizeof name, "SYN:1:FC:%u:%u:%u:%u", 1 + runi(&pr, 8), 1101 + runi(&pr, 1128), runi(&pr, 30000),
+           runi(&pr, 200000));
+  const int lrn = (int)strlen(name) + 1;
+  W32(0);
+  W32(-1);
+  W32(-1);
+  W8(lrn); W8(0); W16(4680);
+  W16(0); W16(second ? 141 : 77);
+  W32(read_len);
+  W32(-1);
+  W32(-1);
+  W32(0);
+  memcpy(rec + n, name, (size_t)lrn); n += lrn;
+  static const uint8_t codes[5] = {1, 2, 4, 8, 15};
+  for (int i = 0; i < read_len; i += 2) {
+    uint8_t hi = codes[runi(r, 5)];
+    uint8_t lo = (i + 1 < read_len) ? codes[runi(r, 5)] : 0;
+    W8((hi << 4) | lo);
+  }
+  for (int i = 0; i < read_len; i++) W8(2 + runi(r, 10));
+  W8('R'); W8('G'); W8('Z'); memcpy(rec + n, "grp1", 5); n += 5;
+  const uint32_t bs = (uint32_t)(n - 4);
+  memcpy(rec, &bs, 4);
+  bput(b, rec, n);
+  co->serial++;
+}
 #undef W32
 #undef W16
 #undef W8
@@ -377,7 +414,13 @@ int64_t synth_tile(uint64_t seed, int64_t target_u, int read_len, int level, int
                    int64_t *n_records, int64_t *u_len) {
   rng_t r = {seed};
   buf_t u = {0};
-  coord_t co = {0, 10000, seed * 1000003ull};
+  coord_t co = {0, 10000, seed * 1000003ull, 0, 1};
+  if (read_len) { /* an equal run of records on each of the 84 contigs */
+    co.per = target_u / ((int64_t)read_len * 2 + 110) / NREF;
+    if (co.per < 1) co.per = 1;
+    co.left = co.per;
+    co.pos = 400;
+  }
   int64_t nrec = 0;
   uint8_t *rec = (uint8_t *)malloc((size_t)(read_len ? 4 * read_len + 4096 : 4 * 50000 + 4 * 3000 + 4096));
   uint32_t *cig = (uint32_t *)malloc(4 * 3008);
@@ -387,6 +430,26 @@ int64_t synth_tile(uint64_t seed, int64_t target_u, int read_len, int level, int
     nrec++;
   }
   free(cig);
+  free(rec);
+  int64_t n = compress_stream(u.p, u.n, level, threads, out);
+  if (n_records) *n_records = nrec;
+  if (u_len) *u_len = u.n;
+  free(u.p);
+  return n;
+}
+
+/* The unplaced tail: ~target_u uncompressed bytes of unmapped pairs without coordinates, compressed. */
+int64_t synth_unplaced(uint64_t seed, int64_t target_u, int read_len, int level, int threads, uint8_t **out,
+                       int64_t *n_records, int64_t *u_len) {
+  rng_t r = {seed ^ 0x0DDBA11ull};
+  buf_t u = {0};
+  coord_t co = {-1, -1, seed * 1000003ull + 1, 0, 1};
+  int64_t nrec = 0;
+  uint8_t *rec = (uint8_t *)malloc((size_t)(4 * read_len + 4096));
+  while (u.n < target_u || (nrec & 1)) {
+    bam_unplaced_record(&u, &r, &co, read_len, rec);
+    nrec++;
+  }
   free(rec);
   int64_t n = compress_stream(u.p, u.n, level, threads, out);
   if (n_records) *n_records = nrec;
