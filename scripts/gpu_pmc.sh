@@ -1,0 +1,13 @@
+# PMC passes on the bench workload (10 GB): HBM traffic (FETCH_SIZE, WRITE_SIZE) and SQ instruction counts, one
+# counter group per pass; summary → gpurun_out/pmc/traffic.json (copy into profiles/<round>/ to use it)
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+OUT=gpurun_out/pmc
+mkdir -p $OUT
+ONLY=${ONLY:-inflate,check_full,check_eager}
+run() { timeout -s KILL 240 rocprofv3 --pmc $2 --output-format csv -d $OUT/$1 -o p -- python3 tools/bench_kernels.py --size-gb 10 --only $ONLY --reps 1 > $OUT/$1.log 2>&1; }
+run f "FETCH_SIZE" || exit 2
+run w "WRITE_SIZE" || exit 3
+run sq1 "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_SMEM" || exit 4
+python3 tools/traffic_pmc.py $OUT/traffic.json $OUT/f $OUT/w --sq-dir $OUT/sq1 > $OUT/summary.log 2>&1 || exit 5
