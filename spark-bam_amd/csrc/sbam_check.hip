@@ -15,6 +15,8 @@
 // time (SWAR).  Positions whose first record passes (true starts and rare near-misses) continue the
 // 10-record chain from global memory.  Counts are accumulated per lane in carry-save bit planes (19 flags)
 // and packed 8-bit key counters, reduced with ballots once per 7 tiles.
+#include <algorithm>
+#include <atomic>
 #include <type_traits>
 
 #include "sbam_internal.h"
@@ -990,6 +992,28 @@ static void interior_tiles(const StreamView &sv, int64_t x0, int64_t x1, int64_t
   *thi = lim - x0a >= kTile ? (lim - x0a) / kTile : 0;
   if (*thi < *tlo) *thi = *tlo;
 }
+// Grid of the grid-stride k_check<MODE, PART> launch: at least the workgroups resident on the whole device.
+template <int MODE, int PART>
+static int resident_grid(int64_t ntiles) {
+  static std::atomic<int> cached[16];
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  int g = cached[dev & 15].load(std::memory_order_relaxed);
+  if (g <= 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_check<MODE, PART>, kCheckThreads, 0) != hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    g = per_cu * cus;
+    cached[dev & 15].store(g, std::memory_order_relaxed);
+  }
+  // many more workgroups than slots, ~40 tiles each: tile costs differ (data, counter flushes), and a slot that
+  // finishes early takes the next workgroup (measured at 10 GB: 1280 → 121 ms, 2048 → 114, 81920 → 99)
+  const int64_t want = std::max<int64_t>(g, std::min<int64_t>(ntiles / 40, 131072));
+  return (int)(ntiles < 1 ? 1 : ntiles < want ? ntiles : want);
+}
+
 // Record-0 pass of mode MODE over [x0, x1): interior tiles by k_check<MODE, 1>, the rest by k_check<MODE, 2>.
 template <int MODE>
 static void launch_split_check(StreamView sv, int64_t x0, int64_t x1, int32_t R, CountsDev cd,
@@ -998,8 +1022,8 @@ static void launch_split_check(StreamView sv, int64_t x0, int64_t x1, int32_t R,
   interior_tiles(sv, x0, x1, &tlo, &thi);
   const int64_t nt = ntiles_of(x0, x1), ni = thi - tlo;
   if (ni > 0)
-    hipLaunchKernelGGL((k_check<MODE, 1>), dim3(check_grid(ni)), dim3(kCheckThreads), 0, s, sv, x0, x1, R, cd, bitmap,
-                       nullptr, tlo, thi);
+    hipLaunchKernelGGL((k_check<MODE, 1>), dim3(resident_grid<MODE, 1>(ni)), dim3(kCheckThreads), 0, s, sv, x0, x1, R,
+                       cd, bitmap, nullptr, tlo, thi);
   if (nt > ni)
     hipLaunchKernelGGL((k_check<MODE, 2>), dim3(check_grid(nt - ni)), dim3(kCheckThreads), 0, s, sv, x0, x1, R, cd,
                        bitmap, nullptr, tlo, thi);
