@@ -665,7 +665,10 @@ int sbam_check_eager(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, uint64_t *b
   if (rc) return rc;
   {
     Timer t(c, "check_eager");
-    HIPCHK(c, launch_check_eager_pass0(view(c), x0, x1, R, c->d_bitmap, c->stream));
+    {
+      Timer t0(c, "check_eager_pass0");
+      HIPCHK(c, launch_check_eager_pass0(view(c), x0, x1, R, c->d_bitmap, c->stream));
+    }
     HIPCHK(c, run_chains(c, x0, x1, R, 0, CountsDev{}));
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -53,6 +53,15 @@ SB_DEV uint32_t wave_sum(uint32_t v) {
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor((int)v, o, 64);
   return v;
 }
+SB_DEV uint32_t wave_incl_scan_u32(uint32_t v) {
+  const int lane = __lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)v, d, 64);
+    if (lane >= d) v += y;
+  }
+  return v;
+}
 SB_DEV uint32_t wave_or(uint32_t v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v |= __shfl_xor((int)v, o, 64);
@@ -583,6 +592,36 @@ SB_DEV uint32_t check_first(const Tile &t, const StreamView &sv, const int32_t *
   return w;
 }
 
+// Stage the window of the tile at `base` (32 B per lane per step) and build the op-class and name-character
+// bitmaps (struct Tile).
+SB_DEV void stage_tile(const StreamView &sv, int64_t base, uint8_t *s_win, uint32_t *s_opc, uint32_t *s_nbad) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) u32x4 *g16;
+  const g16 src = (g16)(gview(sv.u) + base);
+  u32x4 *dst = reinterpret_cast<u32x4 *>(s_win);
+  uint8_t *opc8 = reinterpret_cast<uint8_t *>(s_opc);
+  for (int i = threadIdx.x; i < kWin / 32; i += kCheckThreads) {
+    const u32x4 a = src[2 * i], b = src[2 * i + 1];
+    dst[2 * i] = a;
+    dst[2 * i + 1] = b;
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t cls[4] = {0, 0, 0, 0}, nb = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint32_t inv = inv_nibble(w[j]);  // bit r: byte r of w[j] is an invalid op start
+#pragma unroll
+      for (int r = 0; r < 4; r++) cls[r] |= ((inv >> r) & 1u) << j;
+      const uint32_t m = name_bad_bytes(w[j]);  // bit 7 of each bad byte
+      nb |= (((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u)) << (4 * j);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) opc8[r * 4 * kOpcWords + i] = (uint8_t)cls[r];
+    s_nbad[i] = nb;
+  }
+  if (threadIdx.x < 4) s_nbad[kWin / 32 + threadIdx.x] = 0;
+  if (threadIdx.x < 16) s_opc[(threadIdx.x >> 2) * kOpcWords + kWin / 128 + (threadIdx.x & 3)] = 0;
+}
+
 // ---- the tiled kernel -------------------------------------------------------------------------------------
 enum { MODE_COUNTS = 0, MODE_EAGER = 1, MODE_WORDS = 2, MODE_BYKEY = 3 };
 
@@ -772,33 +811,7 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
     const int64_t t = PART == 1 ? tlo + ti : (ti >= tlo ? ti + nskip : ti);
     const int64_t base = x0a + t * kTile;
     __syncthreads();
-    {  // stage the window (32 B per lane per step) and build the op-class and name-character bitmaps
-      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      typedef const __attribute__((address_space(1))) u32x4 *g16;
-      const g16 src = (g16)(gview(sv.u) + base);
-      u32x4 *dst = reinterpret_cast<u32x4 *>(s_win);
-      uint8_t *opc8 = reinterpret_cast<uint8_t *>(s_opc);
-      for (int i = threadIdx.x; i < kWin / 32; i += kCheckThreads) {
-        const u32x4 a = src[2 * i], b = src[2 * i + 1];
-        dst[2 * i] = a;
-        dst[2 * i + 1] = b;
-        const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-        uint32_t cls[4] = {0, 0, 0, 0}, nb = 0;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-          const uint32_t inv = inv_nibble(w[j]);  // bit r: byte r of w[j] is an invalid op start
-#pragma unroll
-          for (int r = 0; r < 4; r++) cls[r] |= ((inv >> r) & 1u) << j;
-          const uint32_t m = name_bad_bytes(w[j]);  // bit 7 of each bad byte
-          nb |= (((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u)) << (4 * j);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; r++) opc8[r * 4 * kOpcWords + i] = (uint8_t)cls[r];
-        s_nbad[i] = nb;
-      }
-      if (threadIdx.x < 4) s_nbad[kWin / 32 + threadIdx.x] = 0;
-      if (threadIdx.x < 16) s_opc[(threadIdx.x >> 2) * kOpcWords + kWin / 128 + (threadIdx.x & 3)] = 0;
-    }
+    stage_tile(sv, base, s_win, s_opc, s_nbad);
     __syncthreads();
     const Tile tl{s_win, s_opc, s_nbad, base};
     const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
@@ -890,6 +903,132 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
         if (s_k12[i]) atomicAdd(&cd.counts[i], (unsigned long long)s_k12[i]);
     for (int i = threadIdx.x; i < 19 * 19; i += kCheckThreads)
       if (s_pair[i]) atomicAdd(&cd.pair[i], (unsigned long long)s_pair[i]);
+  }
+}
+
+// ---- eager record-0 pass over interior tiles, with a prefilter -------------------------------------------------
+// eager.Checker fails a position at its first failing check, and the first checks are the two reference indices
+// (refIdx, nextRefIdx in [-1, n_ref): PosChecker.scala:43-63, eager/Checker.scala:24-126).  So every position is
+// first tested on those two fields alone (two funnel shifts and two compares per position); only the survivors —
+// true record starts and the few positions whose indices happen to be small — are queued per wave and checked in
+// full (eager_pass_direct, all 64 lanes on queued positions).  Same PASS0 bitmap as k_check<MODE_EAGER, 1>.
+constexpr int kEagerQ = 512;       // per-wave queue of survivors (a tile's are queued in rounds of this many)
+constexpr int kEagerLens = 1024;   // contig lengths in LDS (more: read from HBM) — keeps 8 workgroups per CU
+// eager.Checker at an interior position whose indices passed the prefilter, straight from the staged bytes (no
+// op-class / name-character bitmaps: survivors are few, and a true record's name and CIGAR are short).  Same
+// pass/fail as check_first<true, true>.
+SB_DEV bool eager_pass_direct(const uint8_t *win, const StreamView &sv, const int32_t *lensL, int64_t x, int rel,
+                              const int32_t f[8]) {
+  const int32_t bs = f[0], ri = f[1], rp = f[2], bmn = f[3], fnc = f[4], ls = f[5], nri = f[6], nrp = f[7];
+  const int32_t lrn = bmn & 0xff;
+  const uint32_t flag = ((uint32_t)fnc) >> 16;
+  const int32_t nc = fnc & 0xffff;
+  const uint32_t rb0 = lensL ? ref_bits_lds(ri, rp, lensL, sv.nref) : ref_err(ri, rp, nullptr, sv.lens, sv.nref);
+  const uint32_t rb1 = lensL ? ref_bits_lds(nri, nrp, lensL, sv.nref) : ref_err(nri, nrp, nullptr, sv.lens, sv.nref);
+  if (rb0 | rb1 | (too_few_remaining(bs, lrn, nc, ls) ? 1u : 0u)) return false;
+  if (lrn < 2 || ((flag & 4u) == 0 && (ls == 0 || nc == 0))) return false;
+  if (win[rel + 35 + lrn] != 0) return false;  // name not NUL-terminated
+  for (int i = 0; i < lrn - 1; i++) {
+    const uint32_t c = win[rel + 36 + i];
+    if (!((c - 33u <= 30u) || (c - 65u <= 61u))) return false;  // allowedReadNameChars
+  }
+  const int c0 = rel + 36 + lrn;
+  const int in_win = min(nc, (kWin - c0) >> 2);  // ops inside the staged window, then HBM
+  for (int i = 0; i < in_win; i++)
+    if ((win[c0 + 4 * i] & 0xfu) > 8u) return false;
+  const gbytes u = gview(sv.u);
+  for (int i = in_win; i < nc; i++)
+    if ((u[x + 36 + lrn + 4 * (int64_t)i] & 0xfu) > 8u) return false;
+  return true;
+}
+
+__global__ __launch_bounds__(kCheckThreads) void k_eager(StreamView sv, int64_t x0, int R,
+                                                         unsigned long long *__restrict__ bitmap, int64_t tlo,
+                                                         int64_t thi) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_win[kWin + 64];
+  __shared__ int32_t s_lens[kEagerLens];
+  __shared__ uint16_t s_q[kCheckThreads / 64][kEagerQ];
+  __shared__ unsigned long long s_bits[kTile / 64];
+  const int lane = lane_id(), wv = (int)threadIdx.x >> 6;
+  const int32_t *lensL = nullptr;
+  if (sv.nref <= kEagerLens) {
+    for (int i = threadIdx.x; i < sv.nref; i += kCheckThreads) s_lens[i] = (int32_t)sv.lens[i];
+    lensL = s_lens;
+  }
+  const uint32_t nref1 = (uint32_t)sv.nref;  // idx + 1 <= n_ref  <=>  -1 <= idx < n_ref
+  const int64_t x0a = x0 & ~(int64_t)63;
+  const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
+  uint16_t *q = s_q[wv];
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) u32x4 *g16;
+  // the window of the next tile is loaded into registers while this one is checked
+  constexpr int kPieces = (kWin / 16 + kCheckThreads - 1) / kCheckThreads;
+  u32x4 pre[kPieces];
+  auto fetch = [&](int64_t t) {
+    const g16 src = (g16)(gview(sv.u) + x0a + t * kTile);
+#pragma unroll
+    for (int k = 0; k < kPieces; k++) {
+      const int i = k * kCheckThreads + (int)threadIdx.x;
+      if (i < kWin / 16) pre[k] = src[i];
+    }
+  };
+  if (tlo + (int64_t)blockIdx.x < thi) fetch(tlo + blockIdx.x);
+  for (int64_t t = tlo + blockIdx.x; t < thi; t += gridDim.x) {
+    const int64_t base = x0a + t * kTile;
+    __syncthreads();
+    {
+      u32x4 *dst = reinterpret_cast<u32x4 *>(s_win);
+#pragma unroll
+      for (int k = 0; k < kPieces; k++) {
+        const int i = k * kCheckThreads + (int)threadIdx.x;
+        if (i < kWin / 16) dst[i] = pre[k];
+      }
+    }
+    if (threadIdx.x < kTile / 64) s_bits[threadIdx.x] = 0ull;
+    __syncthreads();
+    if (t + gridDim.x < thi) fetch(t + gridDim.x);
+    // full eager check of the queued positions q[from, from + n), one per lane
+    auto drain = [&](int from, int n) {
+      if (lane < n) {
+        const int rel = q[from + lane];
+        const int o = rel & 3, d = rel >> 2;
+        int32_t f[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) f[k] = (int32_t)__builtin_amdgcn_alignbyte(w32[d + k + 1], w32[d + k], o);
+        if (eager_pass_direct(s_win, sv, lensL, base + rel, rel, f)) atomicOr(&s_bits[rel >> 6], 1ull << (rel & 63));
+      }
+    };
+    // prefilter: bit 4j + o of sm = position 4 (j·kCheckThreads + thread) + o survives
+    uint32_t sm = 0;
+#pragma unroll
+    for (int j = 0; j < kTile / (4 * kCheckThreads); j++) {
+      const int g = j * kCheckThreads + threadIdx.x;  // group of 4 consecutive positions
+      const uint32_t a1 = w32[g + 1], a2 = w32[g + 2], a6 = w32[g + 6], a7 = w32[g + 7];
+#pragma unroll
+      for (int o = 0; o < 4; o++) {
+        const uint32_t ri = __builtin_amdgcn_alignbyte(a2, a1, o), nri = __builtin_amdgcn_alignbyte(a7, a6, o);
+        sm |= (ri + 1u <= nref1 && nri + 1u <= nref1) ? (1u << (4 * j + o)) : 0u;
+      }
+    }
+    // queue the wave's survivors (kEagerQ at a time) and check them 64 at a time
+    const uint32_t n = (uint32_t)__popc(sm);
+    const uint32_t incl = wave_incl_scan_u32(n);
+    const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+    for (uint32_t r0 = 0; r0 < total; r0 += kEagerQ) {
+      uint32_t at = incl - n;
+      for (uint32_t m = sm; m && at < r0 + kEagerQ; m &= m - 1, at++) {
+        if (at >= r0) {
+          const int bit = __builtin_ctz(m);
+          q[at - r0] = (uint16_t)(4 * ((bit >> 2) * kCheckThreads + (int)threadIdx.x) + (bit & 3));
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      const int nq = (int)min((uint32_t)kEagerQ, total - r0);
+      for (int from = 0; from < nq; from += 64) drain(from, min(64, nq - from));
+      __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    if (threadIdx.x < kTile / 64) bitmap[((base - x0a) >> 6) + threadIdx.x] = s_bits[threadIdx.x];
   }
 }
 
@@ -1078,7 +1217,19 @@ hipError_t launch_chain_list_run(StreamView sv, int64_t x0, int64_t x1, int32_t 
 hipError_t launch_check_eager_pass0(StreamView sv, int64_t x0, int64_t x1, int32_t R, unsigned long long *bitmap,
                                     hipStream_t s) {
   if (x1 <= x0) return hipSuccess;
-  launch_split_check<MODE_EAGER>(sv, x0, x1, R, CountsDev{}, bitmap, s);
+  if (R == 0) {  // Success(0) everywhere: no prefilter
+    launch_split_check<MODE_EAGER>(sv, x0, x1, R, CountsDev{}, bitmap, s);
+    return hipGetLastError();
+  }
+  int64_t tlo, thi;
+  interior_tiles(sv, x0, x1, &tlo, &thi);
+  const int64_t nt = ntiles_of(x0, x1), ni = thi - tlo;
+  if (ni > 0)
+    hipLaunchKernelGGL(k_eager, dim3(resident_grid<MODE_EAGER, 1>(ni)), dim3(kCheckThreads), 0, s, sv, x0, (int)R,
+                       bitmap, tlo, thi);
+  if (nt > ni)
+    hipLaunchKernelGGL((k_check<MODE_EAGER, 2>), dim3(check_grid(nt - ni)), dim3(kCheckThreads), 0, s, sv, x0, x1, R,
+                       CountsDev{}, bitmap, nullptr, tlo, thi);
   return hipGetLastError();
 }
 hipError_t launch_check_words(StreamView sv, int64_t x0, int64_t x1, int32_t R, uint32_t *words,

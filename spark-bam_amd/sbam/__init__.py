@@ -423,6 +423,12 @@ class BamFile:
         bits = np.unpackbits(words.view(np.uint8), bitorder="little")
         return bits[: x1 - x0].astype(bool)
 
+    def check_eager_device(self, x0: int = 0, x1: Optional[int] = None,
+                           reads_to_check: int = READS_TO_CHECK) -> None:
+        """check_eager leaving the success bitmap on the device (the split computation reads it there)."""
+        x1 = self.uncompressed_size if x1 is None else x1
+        self._check(self.L.sbam_check_eager(self.ctx, x0, x1, reads_to_check, None))
+
     def check_full_words(self, x0: int = 0, x1: Optional[int] = None,
                          reads_to_check: int = READS_TO_CHECK) -> np.ndarray:
         """full.Checker result words (sbam.h layout) for every offset of [x0, x1)."""
