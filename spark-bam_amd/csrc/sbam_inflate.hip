@@ -715,16 +715,18 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
 // end-of-block or invalid symbol (in the speculative prefix such a symbol is noise): it records up to two such
 // stops and keeps decoding, and phase B decides which, if any, lies on the true path.
 // Block headers are decoded by the whole wave as well: every lane decodes the code-length symbol at one of 64
-// consecutive bit offsets, and the true chain of symbols is followed through those 64 results.  Tables (16-bit
-// entries: a 10-bit root table plus sub-tables for longer codes; 8 bits for distances) are built by the whole
+// consecutive bit offsets, and the true chain of symbols is followed through those 64 results.  Tables (32-bit
+// entries: a 9-bit root table plus sub-tables for longer codes; 8 bits for distances) are built by the whole
 // wave in LDS.  Anything outside the common case — stored or invalid blocks, incomplete codes, a stream that
 // ends before ISIZE or runs past it, a distance too far back — sends the block to k_inflate_slow (the exact
 // per-lane decoder), so zlib's semantics are unchanged.
 namespace wd {
 constexpr int kK = 512;                    // bits per lane segment
 constexpr int kWinDw = 64 * kK / 32 + 16;  // staged input dwords per round (start alignment + lookahead)
-constexpr int kLitRoot = 10, kDistRoot = 8;
-constexpr int kLitSub = 320, kDistSub = 192;  // zlib's ENOUGH: 1332 for 286 symbols at root 10, 400 for 30 at 8
+// A 9-bit literal/length root (zlib's choice: ENOUGH_LENS = 852 entries with sub-tables) keeps the wave's LDS at
+// 9.4 KiB, so 16 decoder waves fit a CU (a 10-bit root: 11.4 KiB, 14 waves, decode 86 → 79 ms at 10 GB).
+constexpr int kLitRoot = 9, kDistRoot = 8;
+constexpr int kLitSub = 344, kDistSub = 192;  // >= ENOUGH - root: 852 - 512 at root 9; 400 - 256 at 8
 constexpr int kLitOff = 0, kDistOff = (1 << kLitRoot) + kLitSub;
 constexpr int kTab = kDistOff + (1 << kDistRoot) + kDistSub;
 constexpr int kCp = 12;            // checkpoints per lane
