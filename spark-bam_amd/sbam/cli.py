@@ -375,7 +375,11 @@ def stats_lines(xs: Sequence[int]) -> List[str]:
 def compute_splits_lines(f: sbam.BamFile, split_size: int, limit: int) -> List[str]:
     t = time.perf_counter()
     splits = f.compute_splits(split_size)
-    ms = int((time.perf_counter() - t) * 1e3)
+    return splits_report(splits, int((time.perf_counter() - t) * 1e3), limit)
+
+
+def splits_report(splits, ms: int, limit: int) -> List[str]:
+    """ComputeSplits.scala:56-68 report text for a list of splits found in `ms` milliseconds."""
     out = [f"Get spark-bam splits: {ms}ms", "", "Split-size distribution:"]
     out += stats_lines([split_length(s) for s in splits])
     out.append("")
@@ -388,8 +392,51 @@ def compute_splits_lines(f: sbam.BamFile, split_size: int, limit: int) -> List[s
 def count_reads_lines(f: sbam.BamFile, split_size: int) -> List[str]:
     t = time.perf_counter()
     n = sum(f.partition_sizes(split_size))
-    ms = int((time.perf_counter() - t) * 1e3)
+    return count_report(n, int((time.perf_counter() - t) * 1e3))
+
+
+def count_report(n: int, ms: int) -> List[str]:
+    """CountReads.scala:80-100 report text (spark-bam side)."""
     return [f"spark-bam read-count time: {ms}", "", f"spark-bam found {n} reads", ""]
+
+
+def spawn_ranks(n: int, argv: Sequence[str]) -> int:
+    """`--gpus N` outside torchrun: N ranks of this command under torch.distributed.run (one per GPU), started
+    before this process touches a GPU."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ)
+    pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env["PYTHONPATH"] = pkg + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "-m", "sbam.cli"] + list(argv)
+    return subprocess.call(cmd, env=env)
+
+
+def sharded_lines(a) -> Optional[List[str]]:
+    """compute-splits / count-reads over byte-range shards, one rank per GPU (sbam.dist.run_file: rank 0 reads the
+    header, each rank preads its shard, one all_gather + all_reduce).  Returns the report on rank 0, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+    from sbam import dist as sdist
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    try:
+        t = time.perf_counter()
+        r = sdist.run_file(a.bam, sbam.effective_split_size(a.max_split_size), device=local,
+                           coll_device=torch.device("cuda", local))
+        ms = int((time.perf_counter() - t) * 1e3)
+        if dist.get_rank() != 0:
+            return None
+        if a.cmd == "compute-splits":
+            return splits_report(r.splits, ms, a.print_limit)
+        return count_report(sum(r.partition_sizes), ms)
+    finally:
+        dist.destroy_process_group()
 
 
 # ---- check-blocks -s / index-blocks / index-records ------------------------------------------------------------
@@ -526,7 +573,20 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
             p.add_argument("-r", "--reads-to-check", type=int, default=10)
         if name in ("compute-splits", "check-bam", "check-blocks"):
             p.add_argument("-s", "--spark-bam", action="store_true")
+        if name in ("compute-splits", "count-reads"):
+            p.add_argument("--gpus", type=int, default=1, help="byte-range shards, one rank per GPU")
     a = ap.parse_args(argv)
+    if getattr(a, "gpus", 1) > 1:
+        if "WORLD_SIZE" not in os.environ:
+            return spawn_ranks(a.gpus, sys.argv[1:] if argv is None else argv)
+        lines = sharded_lines(a)
+        if lines is not None:
+            text = "\n".join(lines) + "\n"
+            if a.out:
+                open(a.out, "w").write(text)
+            else:
+                sys.stdout.write(text)
+        return 0
     data = open(a.bam, "rb").read()
     with sbam.BamFile(data, path=a.bam) as f:
         if a.cmd == "full-check":
