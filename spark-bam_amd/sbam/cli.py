@@ -422,13 +422,17 @@ def sharded_lines(a) -> Optional[List[str]]:
     import torch
     import torch.distributed as dist
     from sbam import dist as sdist
-    local = int(os.environ.get("LOCAL_RANK", 0))
+    local = int(os.environ.get("LOCAL_RANK", 0)) if a.device is None else a.device
     torch.cuda.set_device(local)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if a.dist_backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        coll = torch.device("cuda", local)
+    else:  # gloo: rehearse N ranks on one GPU (--device), small collectives on the host
+        dist.init_process_group(a.dist_backend)
+        coll = None
     try:
         t = time.perf_counter()
-        r = sdist.run_file(a.bam, sbam.effective_split_size(a.max_split_size), device=local,
-                           coll_device=torch.device("cuda", local))
+        r = sdist.run_file(a.bam, sbam.effective_split_size(a.max_split_size), device=local, coll_device=coll)
         ms = int((time.perf_counter() - t) * 1e3)
         if dist.get_rank() != 0:
             return None
@@ -575,6 +579,8 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
             p.add_argument("-s", "--spark-bam", action="store_true")
         if name in ("compute-splits", "count-reads"):
             p.add_argument("--gpus", type=int, default=1, help="byte-range shards, one rank per GPU")
+            p.add_argument("--dist-backend", default="nccl", help="nccl (RCCL); gloo to rehearse ranks on one GPU")
+            p.add_argument("--device", type=int, default=None, help="GPU of every rank (default LOCAL_RANK)")
     a = ap.parse_args(argv)
     if getattr(a, "gpus", 1) > 1:
         if "WORLD_SIZE" not in os.environ:

@@ -194,3 +194,22 @@ def test_split_size_defaults_follow_hadoop():
     finally:
         argparse.ArgumentParser.parse_args = orig
     assert seen == {"compute-splits": None, "count-reads": None, "check-blocks": 2 << 20}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cmd", ["compute-splits", "count-reads"])
+def test_cli_sharded_ranks_match_single(tmp_path, cmd):
+    """`--gpus 2` starts two ranks (torch.distributed.run; gloo on GPU 0 to rehearse on one card) that run
+    sbam.dist.run_file: the report equals the single-GPU one (timing line aside)."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    src = os.path.join(ROOT, "tests", "fixtures", "2.bam")
+    one, two = tmp_path / "one.txt", tmp_path / "two.txt"
+    env = dict(os.environ, PYTHONPATH=os.path.join(ROOT, "spark-bam_amd"))
+    base = [sys.executable, "-m", "sbam.cli", cmd, "-m", "100000", src]
+    subprocess.run(base + [str(one)], check=True, env=env, timeout=100)
+    subprocess.run(base + [str(two), "--gpus", "2", "--dist-backend", "gloo", "--device", "0"], check=True, env=env,
+                   timeout=100)
+    a, b = one.read_text().split("\n"), two.read_text().split("\n")
+    assert a[1:] == b[1:] and len(a) > 3
