@@ -511,7 +511,6 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
   HIPCHK(c, ensure(&c->d_pool, &c->pool_cap, inflate_token_bytes(L, nb)));
   HIPCHK(c, ensure(&c->d_slow, &c->slow_cap, nb));
   if (!c->d_icnt) HIPCHK(c, dalloc(&c->d_icnt, 4));
-  const int res_wgs = (int)std::min<int64_t>((nb + 255) / 256, 256 * 4);
   {
     Timer t(c, "inflate");
     {
@@ -520,7 +519,7 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
                                       c->stream));
     }
     Timer t2(c, "inflate_resolve");
-    HIPCHK(c, launch_inflate_resolve(bt, c->d_u, c->d_pool, d_found, c->d_icnt, res_wgs, c->stream));
+    HIPCHK(c, launch_inflate_resolve(bt, c->d_u, c->d_pool, d_found, c->stream));
   }
   HIPCHK(c, hipMemcpyAsync(c->d_small + 2, &none, 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, launch_first_error(d_status, nb, reinterpret_cast<unsigned long long *>(c->d_small + 2), c->stream));

@@ -7,18 +7,13 @@
 //   * invalid streams (bad block type, stored LEN/NLEN, over-subscribed / incomplete codes, missing EOB code,
 //     bad repeat, invalid symbols, distance too far back) → DATA error; CRC32 is never checked.
 //
-// Design:
-//   k_inflate_decode  — one lane per BGZF block (SIMT across independent blocks).  Huffman decoding is
-//     canonical: per code length l a left-justified limit lim[l] and an index bias bse[l] live in VGPRs,
-//     the symbols in canonical order live in a 640-B LDS slice per lane (256 lanes = all 160 KiB of LDS).
-//     The symbol stream leaves as u16 tokens in 4 KiB pages of an HBM pool (16-B stores; lanes grab pages
-//     with an atomic counter).  No lane ever reads the output, so this kernel never waits on HBM except
-//     for its (prefetched) input dwords.
-//   k_inflate_resolve — one lane per BGZF block again, but with no tables: 1024 lanes per CU hide the
-//     latency of back-reference loads.  Tokens become bytes in a 128-B per-lane LDS ring that leaves as
-//     aligned 64-B groups; copies with distance <= kNear read the ring, longer ones are one unaligned 16-B
-//     load from the output already stored.  A step takes a token plus the literals that follow it (or follow
-//     the copy) in the current chunk.  Overlapping copies double their distance per step.
+// Design, two kernels with the block's "token words" (u32, below) in HBM between them:
+//   k_inflate_wave    — one wavefront per BGZF block: 64 lanes decode 64 consecutive segments of the Huffman
+//     stream speculatively and resynchronise (phases A/B), then write the words of the true path (phase C).
+//     Blocks outside its common case go to k_inflate_slow, the exact per-lane decoder.
+//   k_inflate_resolve — one wavefront per BGZF block: 64 words at a time are placed by a prefix sum and written
+//     into an LDS ring holding the block's recent output; matches resolve in dependency rounds; the output leaves
+//     in 16-B aligned 1 KiB groups.
 #include <type_traits>
 
 #include "sbam_internal.h"
@@ -29,13 +24,18 @@ namespace sbam {
 
 enum : int32_t { INF_OK = 0, INF_SHORT = 1, INF_DATA = 2, INF_OVERFLOW = 3 };
 
-// ---- tokens ---------------------------------------------------------------------------------------------------
-// Token t < 256: literal byte t.  256 <= t < 512: match of length t - 253, followed by the token (distance - 1).
-// 0xffff: padding (the slow decoder keeps a length and its distance in one 16-B chunk).
-constexpr uint32_t kTokPad = 0xffffu;
+// ---- token words ----------------------------------------------------------------------------------------------
+// The decoders hand the resolver one u32 word per match or per run of up to 3 literals, so that every word is
+// self-describing and a wavefront can take 64 words at once:
+//   bit 31 set:   match, bits 16-23 = length - 3, bits 0-14 = distance - 1;
+//   bit 31 clear: bits 24-25 = literal count c (0-3), bytes 0..c-1 = the literals (c = 0: padding).
+// A literal word is closed by a third literal, a length, the end of a decoder lane's segment or the block's end,
+// so a block needs at most 2 B of words per output byte (a 1-literal word is always followed by a match word of
+// >= 3 bytes) — the wave decoder, whose segment ends can add words, checks its count against the region.
+SB_DEV uint32_t tok_match(uint32_t len, uint32_t dist) { return 0x80000000u | ((len - 3u) << 16) | (dist - 1u); }
 
-// Block b's tokens are u16s in the 16-B aligned region tok_region(uoff[b], b) of the token buffer.  A block yields
-// at most ISIZE tokens plus 8 of padding (slow decoder), and regions 2 uoff + 32 b apart never overlap.
+// Block b's words are in the 16-B aligned region tok_region(uoff[b], b) of the token buffer: 2 ISIZE + 32 bytes,
+// regions 2 uoff + 32 b apart never overlap.
 SB_DEV uint64_t tok_region(int64_t uoff, int64_t b) {
   return (((uint64_t)uoff * 2 + 15) & ~15ull) + 32ull * (uint64_t)b;
 }
@@ -212,31 +212,33 @@ SB_DEV uint32_t sel16(const uint32_t (&A)[16], uint32_t i) {
   return csel(m3, csel(m2, u[0], u[1]), csel(m2, u[2], u[3]));
 }
 
-// Token output: an 8-slot shift register (t0 low half = oldest); a full chunk moves to the pending chunk p,
-// which leaves as one 16-B store at the next epoch (so stores issue together with the epoch's loads).
+// Word output: a 4-slot shift register (t0 = oldest) and the open literal word (pw, pc literals); a full chunk
+// moves to the pending chunk p, which leaves as one 16-B store at the next epoch (so stores issue together with
+// the epoch's loads).
 struct TokOut {
   uint32_t t0, t1, t2, t3;
   uint32_t p0, p1, p2, p3;
   int n;
   bool pend;
   uint64_t cur;  // byte offset of the next chunk in the pool
+  uint32_t pw, pc;
 };
 
-// Store one chunk into the block's token region (tok_region: room for every token the block can produce).
+// Store one chunk into the block's token region (tok_region: room for every word the block can produce).
 SB_DEV bool tok_store(TokOut &to, uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint8_t *pool) {
   *reinterpret_cast<uint4 *>(pool + to.cur) = make_uint4(a, b, c, d);
   to.cur += 16;
   return true;
 }
 
-// Append one token; a completed chunk becomes pending (an older pending chunk is stored first: only at a
-// block's end or when more than 8 tokens arrive within one epoch).
+// Append one word; a completed chunk becomes pending (an older pending chunk is stored first: only at a
+// block's end or when more than 4 words arrive within one epoch).
 SB_DEV bool tok_put(TokOut &to, uint32_t t, uint8_t *pool) {
-  to.t0 = __builtin_amdgcn_alignbit(to.t1, to.t0, 16);
-  to.t1 = __builtin_amdgcn_alignbit(to.t2, to.t1, 16);
-  to.t2 = __builtin_amdgcn_alignbit(to.t3, to.t2, 16);
-  to.t3 = __builtin_amdgcn_alignbit(t, to.t3, 16);
-  if (++to.n < 8) return true;
+  to.t0 = to.t1;
+  to.t1 = to.t2;
+  to.t2 = to.t3;
+  to.t3 = t;
+  if (++to.n < 4) return true;
   bool ok = true;
   if (to.pend) ok = tok_store(to, to.p0, to.p1, to.p2, to.p3, pool);
   to.p0 = to.t0;
@@ -246,6 +248,19 @@ SB_DEV bool tok_put(TokOut &to, uint32_t t, uint8_t *pool) {
   to.pend = true;
   to.n = 0;
   return ok;
+}
+SB_DEV bool tok_close_lits(TokOut &to, uint8_t *pool) {
+  if (!to.pc) return true;
+  const uint32_t w = to.pw | (to.pc << 24);
+  to.pw = to.pc = 0;
+  return tok_put(to, w, pool);
+}
+SB_DEV bool tok_lit(TokOut &to, uint32_t byte, uint8_t *pool) {
+  to.pw |= byte << (8 * to.pc);
+  return ++to.pc < 3 ? true : tok_close_lits(to, pool);
+}
+SB_DEV bool tok_put_match(TokOut &to, uint32_t len, uint32_t dist, uint8_t *pool) {
+  return tok_close_lits(to, pool) && tok_put(to, tok_match(len, dist), pool);
 }
 
 enum : int { S_NEXT = 0, S_HDR = 1, S_HUFF = 2, S_STORED = 3, S_DONE = 4, S_EXIT = 5, S_PARK = 6 };
@@ -299,7 +314,7 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
   for (int k = 0; k < 16; k++) A[k] = 0;
 #pragma unroll
   for (int k = 0; k < 8; k++) B[k] = 0;
-  TokOut to{0, 0, 0, 0, 0, 0, 0, 0, 0, false, 0};
+  TokOut to{0, 0, 0, 0, 0, 0, 0, 0, 0, false, 0, 0, 0};
   Canon lc, dc;
   int32_t o = 0, us = 0, err = INF_OK, sleft = 0, fin = 0;
   auto refill = [&]() {  // the symbol loop's refill: next dword from the register window
@@ -335,6 +350,7 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
             to.cur = tok_region(bt.uoff[blk], blk);
             to.n = 0;
             to.pend = false;
+            to.pw = to.pc = 0;
             // word pointer derived from d by arithmetic only (an integer round trip would make it a flat
             // pointer, whose loads the compiler must wait for together with every LDS access)
             const int64_t a = st + hs;
@@ -585,7 +601,7 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
         int len = 0;
         bool is_len = false;
         if (sym < 256) {
-          if (!tok_put(to, (uint32_t)sym, pool)) err = INF_OVERFLOW;
+          if (!tok_lit(to, (uint32_t)sym, pool)) err = INF_OVERFLOW;
           o++;
           if (o == us || err != INF_OK) state = S_DONE;
         } else if (sym == 256) {
@@ -619,7 +635,7 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
           if (!is_len) {
             if (v2 && i2 < h2 && br.left >= L2) {
               br.drop(L2);
-              if (!tok_put(to, (uint32_t)b2, pool)) err = INF_OVERFLOW;
+              if (!tok_lit(to, (uint32_t)b2, pool)) err = INF_OVERFLOW;
               o++;
               if (o == us || err != INF_OK) state = S_DONE;
             }
@@ -645,11 +661,7 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
                   err = INF_DATA;  // invalid distance too far back
                   state = S_DONE;
                 } else {
-                  bool ok = true;
-                  if (to.n == 7) ok = tok_put(to, kTokPad, pool);  // a match never straddles
-                  ok = ok && tok_put(to, (uint32_t)(len + 253), pool);
-                  ok = ok && tok_put(to, (uint32_t)(dist - 1), pool);
-                  if (!ok) err = INF_OVERFLOW;
+                  if (!tok_put_match(to, (uint32_t)len, (uint32_t)dist, pool)) err = INF_OVERFLOW;
                   o = min(o + len, us);
                   if (o == us || err != INF_OK) state = S_DONE;
                 }
@@ -665,7 +677,7 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
       int m = 0;
       for (int i = 0; i < 2; i++) {
         if (i < n && br.left >= 8 && err == INF_OK) {
-          if (!tok_put(to, br.peek(8), pool)) err = INF_OVERFLOW;
+          if (!tok_lit(to, br.peek(8), pool)) err = INF_OVERFLOW;
           br.drop(8);
           m++;
         }
@@ -688,15 +700,16 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
       }
     }
     if (state == S_DONE) {
-      if (err != INF_OVERFLOW) {  // final (padded) chunk and any pending one leave now
-        bool ok = true;
+      if (err != INF_OVERFLOW) {  // the open literal word, the final chunk (padded with empty words) and any
+        bool ok = tok_close_lits(to, pool);  // pending one leave now
         if (to.n > 0)
-          while (ok && to.n > 0) ok = tok_put(to, kTokPad, pool);
+          while (ok && to.n > 0) ok = tok_put(to, 0u, pool);
         if (ok && to.pend) ok = tok_store(to, to.p0, to.p1, to.p2, to.p3, pool);
         if (!ok) err = INF_OVERFLOW;
       }
       to.n = 0;
       to.pend = false;
+      to.pw = to.pc = 0;
       status[blk] = err;
       found[blk] = err == INF_OVERFLOW ? 0 : o;  // an overflowed block has no complete token stream
       state = S_NEXT;
@@ -794,14 +807,26 @@ SB_DEV uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlan
 SB_DEV int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 SB_DEV uint64_t uni(uint64_t x) { return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x); }
 
+// Inclusive prefix sum over the wave: row_shr 1/2/4/8 within rows of 16, then row_bcast 15 / 31 across rows
+// (DPP: no LDS round trip).
 SB_DEV uint32_t wave_incl_scan(uint32_t x) {
-  const int lane = (int)threadIdx.x;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d);
-    if (lane >= d) x += y;
-  }
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
   return x;
+}
+
+// Literal words of the wave decoder (k_inflate_wave): a literal opens a new word unless the open word holds 1 or
+// 2 literals and the previous literal started in the same input dword.  The rule depends only on input positions,
+// so two decodes of one stream that meet at a symbol boundary agree on the words from the next literal that
+// starts a dword on (or the next match) — what phase B's checkpoints need; lit_key is the part of the state that
+// decides the next word there (0: the next literal opens one).
+SB_DEV bool lit_opens(uint32_t pc, uint32_t pq, uint32_t p0) { return pc == 0u || pc == 3u || (p0 >> 5) != pq; }
+SB_DEV uint32_t lit_key(uint32_t pc, uint32_t pq, uint32_t rp) {
+  return (pc == 1u || pc == 2u) && (rp >> 5) == pq ? pc : 0u;
 }
 
 // Decode table of one alphabet from lens[off, off + nsym), by the whole wave, into tab[toff, ...).  Returns false
@@ -1174,7 +1199,8 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       {
         int stt = lane == 0 ? (int)((S >> 9) & 1) : 0;
         uint32_t pl = lane == 0 ? (S & 511u) : 0u;
-        int rp = seg_start;  // reader position
+        uint32_t pc = 0, pq = 0;  // open literal word: literals in it, input dword of the last one (lit_opens)
+        int rp = seg_start;       // reader position
         bool go = true;
         if (seg_start >= pend && lane > 0) {
           go = false;
@@ -1201,18 +1227,23 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
             nst++;
             go = !outp;
           }
-          tokA += stp ? 0u : 1u;
+          // words: a literal that opens one (lit_opens), a distance (its match word)
+          const bool lit = !stp && kind == K_LIT;
+          const bool nw = lit && lit_opens(pc, pq, p0);
+          tokA += (nw || (!stp && kind == K_DIST)) ? 1u : 0u;
           bytA += stp ? 0u : kind == K_LIT ? 1u : kind == K_LEN ? v : 0u;
+          pc = stp ? pc : lit ? (nw ? 1u : pc + 1u) : 0u;
+          pq = lit ? p0 >> 5 : pq;
           pl = (!stp && kind == K_LEN) ? v : pl;
           stt = (!stp && kind == K_LEN) ? 1 : 0;
         };
         // checkpoints every kCpSteps steps (wave-uniform, so a record costs no divergent branch): the lane's
-        // position if it is at a literal/length boundary
+        // position if it is at a literal/length boundary, its counts and its literal-word key there
         sfor<0, kCp>([&](auto J) {
           constexpr int jj = decltype(J)::value;
           const bool live = go && rp < seg_end;
           cp[jj] = (live && stt == 0) ? (uint32_t)rp : ~0u;
-          cc[jj] = tokA | (bytA << 12);
+          cc[jj] = tokA | (bytA << 12) | (lit_key(pc, pq, (uint32_t)rp) << 29);
 #pragma unroll 1
           for (int k = 0; k < kCpSteps; k++)
             if (go && rp < seg_end) step();
@@ -1247,7 +1278,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         WADD(7, 1);
         if (need) {
           int stt = (int)((pex >> 9) & 1);
-          uint32_t pl = pex & 511u, tk = 0, by = 0;
+          uint32_t pl = pex & 511u, tk = 0, by = 0, pc = 0, pq = 0;
           int rp = (int)(pex >> 10);
           // the first checkpoint at or after the reader
           auto next_cp = [&](uint32_t p) {
@@ -1260,9 +1291,13 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
           };
           uint32_t tcp = next_cp((uint32_t)rp);
           for (;;) {
-            if (stt == 0 && (uint32_t)rp == tcp) {  // on the first-pass path from here
-              uint32_t cj = 0;
+            uint32_t cj = 0;
+            if (stt == 0 && (uint32_t)rp == tcp) {
               sfor<0, kCp>([&](auto I) { cj = cp[decltype(I)::value] == tcp ? cc[decltype(I)::value] : cj; });
+            }
+            if (stt == 0 && (uint32_t)rp == tcp && (cj >> 29) == lit_key(pc, pq, (uint32_t)rp)) {
+              // on the first-pass path from here, with the same open literal word: the counts from here on agree
+              cj &= (1u << 29) - 1u;
               const uint32_t P = tcp;
               // the first recorded stop at or after the checkpoint ends the path
               const bool h1 = nst >= 1 && s1p >= P, h2 = !h1 && nst >= 2 && s2p >= P;
@@ -1283,14 +1318,18 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
               break;
             }
             uint32_t v;
+            const uint32_t p0 = (uint32_t)rp;
             const uint32_t kind = (wsym(L, wq, rp, stt, v) >> 8) & 3u;
             const bool outp = rp > pend;
             if (kind == K_SPEC || outp) {
               res = SegResult{tk, by, (uint32_t)rp << 10, outp ? ST_OUT : v == 0 ? ST_EOB : ST_ERR, false};
               break;
             }
-            tk++;
+            const bool nw = kind == K_LIT && lit_opens(pc, pq, p0);
+            tk += (nw || kind == K_DIST) ? 1u : 0u;
             by += kind == K_LIT ? 1u : kind == K_LEN ? v : 0u;
+            pc = kind == K_LIT ? (nw ? 1u : pc + 1u) : 0u;
+            pq = kind == K_LIT ? p0 >> 5 : pq;
             pl = kind == K_LEN ? v : pl;
             stt = kind == K_LEN ? 1 : 0;
             if ((uint32_t)rp > tcp) tcp = next_cp((uint32_t)rp);
@@ -1307,7 +1346,8 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       const uint32_t itok = wave_incl_scan(my_tok), ibyt = wave_incl_scan(my_byt);
       const uint32_t tot_tok = uni((uint32_t)__shfl(itok, 63)), tot_byt = uni((uint32_t)__shfl(ibyt, 63));
       const int stop_f = f < 64 ? uni(__shfl(res.stop, f)) : ST_NONE;
-      if (stop_f == ST_ERR || stop_f == ST_OUT || out + (int)tot_byt > us || __ballot(act && res.bad) != 0) {
+      if (stop_f == ST_ERR || stop_f == ST_OUT || out + (int)tot_byt > us || __ballot(act && res.bad) != 0 ||
+          4 * (ntok + (int)tot_tok) > 2 * us + 32) {  // (words past the region: only a pathological stream)
         ok = false;
         break;
       }
@@ -1321,18 +1361,27 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         int rp = (int)(start >> 10);
         int o = out + (int)(ibyt - my_byt);
         uint32_t ti = (uint32_t)ntok + (itok - my_tok);
+        uint32_t pw = 0, pc = 0, pq = 0;  // open literal word
+        uint32_t *rw = reinterpret_cast<uint32_t *>(reg);
         while (rp < seg_end) {
           uint32_t v;
+          const uint32_t p0 = (uint32_t)rp;
           const uint32_t kind = (wsym(L, wq, rp, stt, v) >> 8) & 3u;
           if (kind == K_SPEC) break;  // the end-of-block symbol of lane f
-          const uint32_t t = kind == K_LIT ? v : kind == K_LEN ? v + 253u : v - 1u;
-          if (kind == K_DIST) derr |= (int)v > o - (int)pl;
+          // at most one word leaves per symbol: the open literal word when this symbol closes it (a literal that
+          // opens a new word, or a length), or the match word at its distance
+          const bool lit = kind == K_LIT, dist = kind == K_DIST;
+          const bool nw = lit && lit_opens(pc, pq, p0);
+          if ((pc != 0u && (nw || !lit)) || dist) rw[ti++] = dist ? tok_match(pl, v) : pw | (pc << 24);
+          derr |= dist && (int)v > o - (int)pl;
+          pw = lit ? (nw ? v : pw | (v << (8 * pc))) : 0u;
+          pc = lit ? (nw ? 1u : pc + 1u) : 0u;
+          pq = lit ? p0 >> 5 : pq;
           o += kind == K_LIT ? 1 : kind == K_LEN ? (int)v : 0;
           pl = kind == K_LEN ? v : pl;
           stt = kind == K_LEN ? 1 : 0;
-          *reinterpret_cast<uint16_t *>(reg + 2 * ti) = (uint16_t)t;
-          ti++;
         }
+        if (pc) rw[ti] = pw | (pc << 24);
       }
       WMARK(5);
       if (__ballot(derr) != 0) { ok = false; break; }
@@ -1362,225 +1411,188 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
 }
 
 // ---- resolve kernel -------------------------------------------------------------------------------------------
-// One lane per BGZF block.  Both of its HBM streams are shaped for the memory side, which bounds this kernel:
-// with every block in flight, a lane's share of L2 is tens of bytes, so a 16-B access to a line costs the whole
-// line.  Tokens are read 128 B (64 tokens) at a time; output leaves in 64-B aligned groups of four 16-B stores
-// (the line is written whole while it is still in L2); a far copy is one unaligned 16-B load.
-constexpr int kResThreads = 256;
-constexpr int kResRing = 136;  // per-lane ring stride (128 B used): 34 dwords, 8-B aligned
-// Copies with (effective) distance <= kNear read the ring, longer ones HBM.  Ring invariants (128-B ring):
-//  * the flushed mark trails the output by <= 63 B when a step starts, and a copy step writes 16 bytes at the
-//    output, so a far copy's 16-B source [a - eff, a - eff + 16) lies below the flushed mark when eff >= 63 + 16
-//    = 79, i.e. for every eff > kNear;
-//  * a step advances the output by at most 16 + kResLits - 1 (a copy, then the literals after it) and writes
-//    ring bytes up to 3 past that (the dword-aligned 16-B scratch write), so the bytes it touches stay clear of
-//    the kNear-byte window a near copy reads behind the output and of the unflushed group.
-constexpr int kNear = 80;
-constexpr int kResLits = 4;  // literals a step may take (the first token plus up to kResLits - 1 more)
-static_assert(63 + 16 <= kNear + 1, "far copies read only flushed output");
-static_assert(kNear + 16 + kResLits + 3 <= 128, "a step's ring writes never reach the near window");
+// One wavefront per BGZF block; the block's recent output lives in a kRing-byte LDS ring (ring byte of output
+// position p: (uoff + p) mod kRing, so ring chunks and HBM chunks share their 16-B alignment).  A step ("chunk")
+// takes the next 64 words, one per lane:
+//   1. a wave prefix sum of the words' output lengths gives every word its position O (a chunk is cut where a word
+//      would start kSpan or more bytes after the chunk's base, and at the block's end);
+//   2. the ring dwords the chunk will write are zeroed, then every byte is written by an LDS OR of its (masked,
+//      shifted) dword — lanes writing neighbouring bytes of one dword never race;
+//   3. literal words are written at once; matches go in rounds: a match is ready when its source ends at or before
+//      the first pending match of the chunk (the first pending one always is), ready matches copy in steps of up
+//      to 16 bytes (an overlapping copy doubles its distance per step) from the ring (distance <= kNear) or, for
+//      far sources, from the output already flushed to HBM;
+//   4. completed output leaves in 1 KiB groups of 16-B aligned stores; a block's partial first and last 16-B chunks
+//      (shared with its neighbours) leave as byte stores.
+// A block's LZ77 window never leaves the chip except for the far copies; HBM sees the words once and the output
+// once.  (Round 2; the round-1 design ran one lane per block with the window in HBM and was bound by the memory
+// side: 16.5x the output bytes per launch.)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+namespace rs {
+constexpr int kSpan = 1024;   // a chunk's words start within kSpan bytes of its base
+constexpr int kFlush = 1024;  // output bytes per group store (64 lanes x 16 B)
+}  // namespace rs
 
-// Tokens are read a group of kTG 16-B chunks at a time from the block's (16-B aligned) token region.
-constexpr int kTokGroup = 128;
-constexpr int kTG = kTokGroup / 16;  // chunks per token group
-static_assert(kTG >= 2, "a group holds the current chunk and at least one more");
-
-struct TokIn {
-  uint32_t t0, t1, t2, t3;      // current chunk (t0 low half = next token)
-  uint32_t q[4 * (kTG - 1)];    // up to kTG - 1 more chunks
-  int n;                        // tokens left in t0..t3
-  int nq;                       // chunks left in q
-  uint64_t cur;                 // byte offset of the next group in the token buffer
-  SB_DEV void load(const uint8_t *pool) {
-    const uint4 *g = reinterpret_cast<const uint4 *>(pool + cur);
-    uint4 c[kTG];
-#pragma unroll
-    for (int k = 0; k < kTG; k++) c[k] = g[k];
-#pragma unroll
-    for (int k = 1; k < kTG; k++) {
-      q[4 * (k - 1) + 0] = c[k].x; q[4 * (k - 1) + 1] = c[k].y;
-      q[4 * (k - 1) + 2] = c[k].z; q[4 * (k - 1) + 3] = c[k].w;
-    }
-    t0 = c[0].x; t1 = c[0].y; t2 = c[0].z; t3 = c[0].w;
-    nq = kTG;  // (t counts as the first)
-    cur += 16 * kTG;
-  }
-  SB_DEV uint32_t get(const uint8_t *pool) {
-    if (n == 0) {
-      if (nq == 0) load(pool);
-      if (nq == kTG) {
-        nq = kTG - 1;
-      } else {
-        t0 = q[0]; t1 = q[1]; t2 = q[2]; t3 = q[3];
-#pragma unroll
-        for (int k = 0; k < 4 * (kTG - 2); k++) q[k] = q[k + 4];
-        nq--;
-      }
-      n = 8;
-    }
-    const uint32_t t = t0 & 0xffffu;
-    t0 = __builtin_amdgcn_alignbit(t1, t0, 16);
-    t1 = __builtin_amdgcn_alignbit(t2, t1, 16);
-    t2 = __builtin_amdgcn_alignbit(t3, t2, 16);
-    t3 >>= 16;
-    n--;
-    return t;
-  }
+template <int RB>
+struct RingGeom {
+  static constexpr uint32_t kRing = 1u << RB, kMask = kRing - 1u, kDw = kRing / 4u, kDwMask = kDw - 1u;
+  // Near sources: the ring holds positions (E + 3 - kRing, E) while a chunk ending at E <= base + kSpan + 257 is
+  // written, so every source at distance <= kNear from a word starting before base + kSpan is intact.
+  static constexpr int kNear = (int)kRing - rs::kSpan - 264;
+  // A far copy's 16-B loads end before O - d + L + 15 < base + kSpan + 272 - d, and the flushed mark is past
+  // base - kFlush: distance >= kSpan + kFlush + 272 keeps them in HBM-resident output.
+  static_assert(kNear >= rs::kSpan + rs::kFlush + 272, "far sources are in HBM");
+  // A slot is flushed before a later chunk zeroes it: kRing > kSpan + 260 + kFlush.
+  static_assert((int)kRing > rs::kSpan + 260 + rs::kFlush, "slots are flushed before reuse");
 };
 
-__global__ __launch_bounds__(kResThreads, 4) void k_inflate_resolve(BlockTable bt, uint8_t *__restrict__ out,
-                                                                    const uint8_t *__restrict__ pool,
-                                                                    const int32_t *__restrict__ found,
-                                                                    unsigned int *next_block) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_ring[kResThreads * kResRing];
-  uint8_t *ring = s_ring + threadIdx.x * kResRing;
-  uint32_t *ring32 = reinterpret_cast<uint32_t *>(ring);
+// OR up to 5 dwords into the ring at dword q (wrapping).  The common case uses immediate offsets.
+template <class G>
+SB_DEV void ring_or5(uint32_t *ring, uint32_t q, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4) {
+  if (q + 4u < G::kDw) {
+    uint32_t *p = ring + q;
+    atomicOr(p + 0, w0);
+    atomicOr(p + 1, w1);
+    atomicOr(p + 2, w2);
+    atomicOr(p + 3, w3);
+    atomicOr(p + 4, w4);
+  } else {
+    atomicOr(ring + (q & G::kDwMask), w0);
+    atomicOr(ring + ((q + 1u) & G::kDwMask), w1);
+    atomicOr(ring + ((q + 2u) & G::kDwMask), w2);
+    atomicOr(ring + ((q + 3u) & G::kDwMask), w3);
+    atomicOr(ring + ((q + 4u) & G::kDwMask), w4);
+  }
+}
 
-  // positions are byte offsets into `out` (kept as offsets so every access stays a global, not flat, access;
-  // `out` is 256-B aligned, so offset alignment is address alignment)
-  bool active = false, exited = false;
-  int64_t a = 0, ae = 0, fl = 0;
-  TokIn ti;
-  ti.t0 = ti.t1 = ti.t2 = ti.t3 = 0;
-#pragma unroll
-  for (int k = 0; k < 4 * (kTG - 1); k++) ti.q[k] = 0;
-  ti.n = ti.nq = 0;
-  ti.cur = 0;
-  int crem = 0, eff = 0, npad = 0;
-  auto flush16 = [&](int64_t x) {  // the aligned 16-B chunk at x (ring stride is 8-B aligned)
-    const uint2 lo = *reinterpret_cast<const uint2 *>(ring + (x & 127));
-    const uint2 hi = *reinterpret_cast<const uint2 *>(ring + ((x + 8) & 127));
-    *reinterpret_cast<uint4 *>(out + x) = make_uint4(lo.x, lo.y, hi.x, hi.y);
-  };
-
-  for (;;) {
-    if (!active && !exited) {
-      const int64_t b = (int64_t)atomicAdd(next_block, 1u);
-      if (b >= bt.n) {
-        exited = true;
-      } else {
-        const int32_t f = found[b];
-        if (f > 0) {
-          a = bt.uoff[b];
-          ae = a + f;
-          fl = a;
-          ti.n = ti.nq = 0;
-          ti.cur = tok_region(bt.uoff[b], b);
-          crem = 0;
-          npad = 0;
-          active = true;
+template <int RB>
+__global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *__restrict__ out,
+                                                        const uint8_t *__restrict__ pool,
+                                                        const int32_t *__restrict__ found) {
+  using G = RingGeom<RB>;
+  __shared__ __attribute__((aligned(16))) uint32_t ring[G::kDw];
+  uint8_t *ring8 = reinterpret_cast<uint8_t *>(ring);
+  const int lane = (int)threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const int ae = found[b];  // output bytes of the block
+  if (ae <= 0) return;
+  const int64_t U0 = bt.uoff[b];
+  uint8_t *ob = out + U0;
+  const uint32_t Gr = (uint32_t)U0 & G::kMask;  // ring byte of position 0
+  const uint32_t *wp = reinterpret_cast<const uint32_t *>(pool + tok_region(U0, b));
+  const int F0 = (int)((16 - (U0 & 15)) & 15);  // first position on a 16-B boundary
+  int F = F0;                                     // flushed up to here (from F0)
+  bool head = F0 == 0;                            // positions [0, F0) stored
+  int Z = -(int)(Gr & 3u);                        // ring zeroed for positions [.., Z); Gr + Z is dword aligned
+  int B = 0, wi = 0;
+  uint32_t w = wp[lane];
+  while (B < ae) {
+    // ---- 1. positions
+    const bool isM = (int32_t)w < 0;
+    const int Lw = isM ? (int)((w >> 16) & 255u) + 3 : (int)((w >> 24) & 3u);
+    const int incl = (int)wave_incl_scan((uint32_t)Lw);
+    const int ex = incl - Lw;
+    const int O = B + ex;
+    const bool take = ex < rs::kSpan && O < ae;
+    const int nt = __popcll(__ballot(take));  // a prefix of the lanes (lane 0 always)
+    const int E = min(B + __builtin_amdgcn_readlane(incl, nt - 1), ae);
+    const int wi2 = uni(wi + nt);
+    const uint32_t wn = wp[wi2 + lane];  // next chunk's words (reads past the stream stay inside the pool)
+    // ---- 2. zero the ring dwords of [Z, E)
+    {
+      const uint32_t z0 = (Gr + (uint32_t)Z) >> 2, z1 = (Gr + (uint32_t)E + 3u) >> 2;
+      for (uint32_t k = z0 + (uint32_t)lane; k < z1; k += 64u) ring[k & G::kDwMask] = 0u;
+      Z = (int)(z1 * 4u - Gr);
+    }
+    const int Le = take ? min(Lw, ae - O) : 0;
+    // ---- 3a. literal words
+    if (take && !isM && Le > 0) {
+      const uint32_t v = w & (Le >= 3 ? 0xffffffu : Le == 2 ? 0xffffu : 0xffu);
+      const uint32_t x = (Gr + (uint32_t)O) & G::kMask, q = x >> 2, s8 = (x & 3u) * 8u;
+      const uint64_t sv = (uint64_t)v << s8;
+      atomicOr(ring + q, (uint32_t)sv);
+      if ((uint32_t)(sv >> 32)) atomicOr(ring + ((q + 1u) & G::kDwMask), (uint32_t)(sv >> 32));
+    }
+    // ---- 3b. matches, in rounds
+    const int d = (int)(w & 0x7fffu) + 1;
+    const bool mt = take && isM && Le > 0;
+    const bool far = d > G::kNear;
+    const int srcEnd = O - d + min(Le, d);
+    uint64_t pend = __ballot(mt);
+    while (pend) {
+      const int f = __ffsll((unsigned long long)pend) - 1;
+      const int fr = __builtin_amdgcn_readlane(O, f);
+      const uint64_t ready = pend & __ballot(srcEnd <= fr);
+      if ((ready >> lane) & 1ull) {
+        int done = 0, deff = d;
+        while (done < Le) {
+          const int n = min(min(Le - done, 16), deff);
+          const int src = O + done - deff;
+          uint32_t v0, v1, v2, v3;
+          if (far) {  // below the flushed mark: one unaligned 16-B load, past this CU's L1 (nt)
+            const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(ob + src));
+            v0 = x.x; v1 = x.y; v2 = x.z; v3 = x.w;
+          } else {
+            const uint32_t xs = (Gr + (uint32_t)src) & G::kMask, qs = xs >> 2, ss = xs & 3u;
+            uint32_t s0, s1, s2, s3, s4;
+            if (qs + 4u < G::kDw) {
+              const uint32_t *p = ring + qs;
+              s0 = p[0]; s1 = p[1]; s2 = p[2]; s3 = p[3]; s4 = p[4];
+            } else {
+              s0 = ring[qs];
+              s1 = ring[(qs + 1u) & G::kDwMask];
+              s2 = ring[(qs + 2u) & G::kDwMask];
+              s3 = ring[(qs + 3u) & G::kDwMask];
+              s4 = ring[(qs + 4u) & G::kDwMask];
+            }
+            v0 = __builtin_amdgcn_alignbyte(s1, s0, ss);
+            v1 = __builtin_amdgcn_alignbyte(s2, s1, ss);
+            v2 = __builtin_amdgcn_alignbyte(s3, s2, ss);
+            v3 = __builtin_amdgcn_alignbyte(s4, s3, ss);
+          }
+          // keep the first n bytes
+          const uint32_t nb = (uint32_t)n * 8u;
+          const uint64_t mlo = nb >= 64u ? ~0ull : (1ull << nb) - 1ull;
+          const uint64_t mhi = nb <= 64u ? 0ull : nb >= 128u ? ~0ull : (1ull << (nb - 64u)) - 1ull;
+          v0 &= (uint32_t)mlo;
+          v1 &= (uint32_t)(mlo >> 32);
+          v2 &= (uint32_t)mhi;
+          v3 &= (uint32_t)(mhi >> 32);
+          // shift to the destination's byte offset and OR in
+          const uint32_t xd = (Gr + (uint32_t)(O + done)) & G::kMask, qd = xd >> 2, s8 = (xd & 3u) * 8u;
+          const uint64_t a01 = ((uint64_t)v1 << 32 | v0) << s8, a12 = ((uint64_t)v2 << 32 | v1) << s8,
+                         a23 = ((uint64_t)v3 << 32 | v2) << s8, a34 = (uint64_t)v3 << s8;
+          ring_or5<G>(ring, qd, (uint32_t)a01, (uint32_t)(a01 >> 32), (uint32_t)(a12 >> 32), (uint32_t)(a23 >> 32),
+                      (uint32_t)(a34 >> 32));
+          done += n;
+          if (n == deff && deff < 16) deff *= 2;  // the copied bytes extend the period: 2·deff is a valid distance
         }
       }
+      pend &= ~ready;
     }
-    if (__all(exited)) break;
-    if (!active) continue;
-
-    if (crem == 0) {
-      const uint32_t t = ti.get(pool);
-      if (t < 256) {
-        ring[a & 127] = (uint8_t)t;
-        a++;
-        // more literals of a run, up to kResLits per step, from the current chunk
-#pragma unroll
-        for (int k = 1; k < kResLits; k++) {
-          const uint32_t t2 = ti.t0 & 0xffffu;
-          if (!(ti.n > 0 && t2 < 256 && a < ae)) break;
-          ring[a & 127] = (uint8_t)t2;
-          a++;
-          ti.get(pool);
-        }
-      } else if (t != kTokPad) {
-        crem = (int)t - 253;
-        eff = (int)ti.get(pool) + 1;
-      }
-      npad = t == kTokPad ? npad + 1 : 0;
-      if (npad > 8) active = false;  // never for a decoded stream: a guard against reading past its end
+    // ---- 4. output
+    B = E;
+    if (!head && B >= F0) {  // the block's first partial 16-B chunk (shared with the previous block)
+      if (lane < F0) ob[lane] = ring8[(Gr + (uint32_t)lane) & G::kMask];
+      head = true;
     }
-    if (crem > 0) {
-      const int n = min(min(crem, 16), min(eff, (int)(ae - a)));
-      const int64_t src = a - eff;
-      uint32_t v0, v1, v2, v3;
-      if (eff <= kNear) {  // source in the ring: 5 dwords around it
-        const int sh = (int)(src & 3);
-        const int q = (int)((src & 127) >> 2);
-        const uint32_t s0 = ring32[q & 31], s1 = ring32[(q + 1) & 31], s2 = ring32[(q + 2) & 31],
-                       s3 = ring32[(q + 3) & 31], s4 = ring32[(q + 4) & 31];
-        v0 = __builtin_amdgcn_alignbyte(s1, s0, sh);
-        v1 = __builtin_amdgcn_alignbyte(s2, s1, sh);
-        v2 = __builtin_amdgcn_alignbyte(s3, s2, sh);
-        v3 = __builtin_amdgcn_alignbyte(s4, s3, sh);
-      } else {  // source already stored to HBM (it lies below the flushed mark): one unaligned 16-B load
-        const uint4 x = *reinterpret_cast<const uint4 *>(out + src);
-        v0 = x.x;
-        v1 = x.y;
-        v2 = x.z;
-        v3 = x.w;
-      }
-      // write 16 bytes at a (bytes past a + n are scratch, rewritten before they are flushed):
-      // head bytes up to the next dword boundary, then 4 aligned dwords
-      const int h = (int)((4 - (a & 3)) & 3);
-#pragma unroll
-      for (int k = 0; k < 3; k++)
-        if (k < h) ring[(a + k) & 127] = (uint8_t)(v0 >> (8 * k));
-      const uint32_t w0 = __builtin_amdgcn_alignbyte(v1, v0, h), w1 = __builtin_amdgcn_alignbyte(v2, v1, h),
-                     w2 = __builtin_amdgcn_alignbyte(v3, v2, h), w3 = __builtin_amdgcn_alignbyte(0u, v3, h);
-      const int q = (int)(((a + h) & 127) >> 2);
-      ring32[q & 31] = w0;
-      ring32[(q + 1) & 31] = w1;
-      ring32[(q + 2) & 31] = w2;
-      ring32[(q + 3) & 31] = w3;
-      a += n;
-      crem -= n;
-      if (n == eff && eff < 16) eff *= 2;  // the copied bytes extend the period: distance 2·eff is valid
+    while (B - F >= rs::kFlush) {
+      const uint32_t x = (Gr + (uint32_t)(F + 16 * lane)) & G::kMask;  // 16-B aligned
+      *reinterpret_cast<uint4 *>(ob + F + 16 * lane) = *reinterpret_cast<const uint4 *>(ring8 + x);
+      F += rs::kFlush;
     }
-    if (crem == 0) {  // literals that follow the copy (or the step's literals), from the current chunk
-#pragma unroll
-      for (int k = 1; k < kResLits; k++) {
-        const uint32_t t2 = ti.t0 & 0xffffu;
-        if (!(ti.n > 0 && t2 < 256 && a < ae)) break;
-        ring[a & 127] = (uint8_t)t2;
-        a++;
-        ti.get(pool);
-      }
-    }
-    // flush: a block's partial first chunk (shared with the previous block) as bytes, then aligned 16-B
-    // chunks up to a 64-B boundary, then whole 64-B groups
-    if (fl & 15) {
-      const int64_t hd = (fl & ~(int64_t)15) + 16;
-      if (a >= hd || a == ae) {
-        const int64_t lim = a < hd ? a : hd;
-        for (int64_t x = fl; x < lim; x++) out[x] = ring[x & 127];
-        fl = lim;
-      }
-    }
-    if ((fl & 15) == 0) {
-      if ((fl & 63) == 0) {
-        if (a - fl >= 64) {
-          const uint2 *r = reinterpret_cast<const uint2 *>(ring + (fl & 127));
-          const uint2 x0 = r[0], x1 = r[1], x2 = r[2], x3 = r[3], x4 = r[4], x5 = r[5], x6 = r[6], x7 = r[7];
-          uint4 *o = reinterpret_cast<uint4 *>(out + fl);
-          o[0] = make_uint4(x0.x, x0.y, x1.x, x1.y);
-          o[1] = make_uint4(x2.x, x2.y, x3.x, x3.y);
-          o[2] = make_uint4(x4.x, x4.y, x5.x, x5.y);
-          o[3] = make_uint4(x6.x, x6.y, x7.x, x7.y);
-          fl += 64;
-        }
-      } else {
-        while ((fl & 63) != 0 && a - fl >= 16) {
-          flush16(fl);
-          fl += 16;
-        }
-      }
-    }
-    if (a == ae) {  // tail (shared with the next block): whole 16-B chunks, then bytes
-      while (ae - fl >= 16) {
-        flush16(fl);
-        fl += 16;
-      }
-      for (int64_t x = fl; x < ae; x++) out[x] = ring[x & 127];
-      fl = ae;
-      active = false;
-    }
+    w = wn;
+    wi = wi2;
+  }
+  // tail: the head (a block shorter than its first partial chunk), whole 16-B chunks, the last partial chunk
+  if (!head) {
+    if (lane < min(F0, ae)) ob[lane] = ring8[(Gr + (uint32_t)lane) & G::kMask];
+  }
+  if (ae > F0) {
+    const int Ft = F + ((ae - F) & ~15);
+    for (int p = F + 16 * lane; p < Ft; p += rs::kFlush)
+      *reinterpret_cast<uint4 *>(ob + p) = *reinterpret_cast<const uint4 *>(ring8 + ((Gr + (uint32_t)p) & G::kMask));
+    if (Ft + lane < ae) ob[Ft + lane] = ring8[(Gr + (uint32_t)(Ft + lane)) & G::kMask];
   }
 }
 
@@ -1599,7 +1611,7 @@ hipError_t launch_first_error(const int32_t *status, int64_t n, unsigned long lo
 hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *tok, int32_t *status,
                                  int32_t *found, int32_t *slow, unsigned int *counters, hipStream_t s) {
   if (bt.n == 0) return hipSuccess;
-  // counters: [0] slow-path blocks, [1] slow-path work, [2] resolve work
+  // counters: [0] slow-path blocks, [1] slow-path work
   (void)hipMemsetAsync(counters, 0, 3 * sizeof(unsigned int), s);
   hipLaunchKernelGGL(k_inflate_wave, dim3((unsigned)bt.n), dim3(64), 0, s, d, D, bt, tok, status, found, slow,
                      counters + 0);
@@ -1609,10 +1621,10 @@ hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, uin
 }
 
 hipError_t launch_inflate_resolve(BlockTable bt, uint8_t *out, const uint8_t *tok, const int32_t *found,
-                                  unsigned int *counters, int res_wgs, hipStream_t s) {
+                                  hipStream_t s) {
   if (bt.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_inflate_resolve, dim3((unsigned)res_wgs), dim3(kResThreads), 0, s, bt, out, tok, found,
-                     counters + 2);
+  // a 4 KiB ring: 8 waves per SIMD (an 8 KiB ring, 5 per SIMD: 58 ms at 10 GB; 4 KiB: 46 ms)
+  hipLaunchKernelGGL(k_inflate_resolve<12>, dim3((unsigned)bt.n), dim3(64), 0, s, bt, out, tok, found);
   return hipGetLastError();
 }
 

@@ -77,7 +77,7 @@ inline size_t inflate_token_bytes(int64_t L, int64_t nb) {
 hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *tok, int32_t *status,
                                  int32_t *found, int32_t *slow, unsigned int *counters, hipStream_t s);
 hipError_t launch_inflate_resolve(BlockTable bt, uint8_t *out, const uint8_t *tok, const int32_t *found,
-                                  unsigned int *counters, int res_wgs, hipStream_t s);
+                                  hipStream_t s);
 // first_err = min block index with status != 0 (caller presets ~0)
 hipError_t launch_first_error(const int32_t *status, int64_t n, unsigned long long *first_err, hipStream_t s);
 hipError_t launch_lower_bound(const Candidate *c, int64_t n, int64_t q, int64_t *out, hipStream_t s);
