@@ -24,18 +24,14 @@ namespace sbam {
 
 enum : int32_t { INF_OK = 0, INF_SHORT = 1, INF_DATA = 2, INF_OVERFLOW = 3 };
 
-// ---- token words ----------------------------------------------------------------------------------------------
-// The decoders hand the resolver one u32 word per match or per run of up to 3 literals, so that every word is
-// self-describing and a wavefront can take 64 words at once:
-//   bit 31 set:   match, bits 16-23 = length - 3, bits 0-14 = distance - 1;
-//   bit 31 clear: bits 24-25 = literal count c (0-3), bytes 0..c-1 = the literals (c = 0: padding).
-// A literal word is closed by a third literal, a length, the end of a decoder lane's segment or the block's end,
-// so a block needs at most 2 B of words per output byte (a 1-literal word is always followed by a match word of
-// >= 3 bytes) — the wave decoder, whose segment ends can add words, checks its count against the region.
-SB_DEV uint32_t tok_match(uint32_t len, uint32_t dist) { return 0x80000000u | ((len - 3u) << 16) | (dist - 1u); }
+// ---- tokens ---------------------------------------------------------------------------------------------------
+// u16 tokens, each self-describing so that the resolver can take 128 at once: t < 256 literal byte t;
+// 256 <= t < 512 length t - 253, followed by its distance token 0x8000 | (distance - 1); kTokPad: padding.
+constexpr uint32_t kTokPad = 0x7fffu;
+constexpr uint32_t kTokDist = 0x8000u;
 
-// Block b's words are in the 16-B aligned region tok_region(uoff[b], b) of the token buffer: 2 ISIZE + 32 bytes,
-// regions 2 uoff + 32 b apart never overlap.
+// Block b's tokens are u16s in the 16-B aligned region tok_region(uoff[b], b) of the token buffer.  A block yields
+// at most ISIZE tokens plus 7 of padding (slow decoder), and regions 2 uoff + 32 b apart never overlap.
 SB_DEV uint64_t tok_region(int64_t uoff, int64_t b) {
   return (((uint64_t)uoff * 2 + 15) & ~15ull) + 32ull * (uint64_t)b;
 }
@@ -212,33 +208,31 @@ SB_DEV uint32_t sel16(const uint32_t (&A)[16], uint32_t i) {
   return csel(m3, csel(m2, u[0], u[1]), csel(m2, u[2], u[3]));
 }
 
-// Word output: a 4-slot shift register (t0 = oldest) and the open literal word (pw, pc literals); a full chunk
-// moves to the pending chunk p, which leaves as one 16-B store at the next epoch (so stores issue together with
-// the epoch's loads).
+// Token output: an 8-slot shift register (t0 low half = oldest); a full chunk moves to the pending chunk p,
+// which leaves as one 16-B store at the next epoch (so stores issue together with the epoch's loads).
 struct TokOut {
   uint32_t t0, t1, t2, t3;
   uint32_t p0, p1, p2, p3;
   int n;
   bool pend;
   uint64_t cur;  // byte offset of the next chunk in the pool
-  uint32_t pw, pc;
 };
 
-// Store one chunk into the block's token region (tok_region: room for every word the block can produce).
+// Store one chunk into the block's token region (tok_region: room for every token the block can produce).
 SB_DEV bool tok_store(TokOut &to, uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint8_t *pool) {
   *reinterpret_cast<uint4 *>(pool + to.cur) = make_uint4(a, b, c, d);
   to.cur += 16;
   return true;
 }
 
-// Append one word; a completed chunk becomes pending (an older pending chunk is stored first: only at a
-// block's end or when more than 4 words arrive within one epoch).
+// Append one token; a completed chunk becomes pending (an older pending chunk is stored first: only at a
+// block's end or when more than 8 tokens arrive within one epoch).
 SB_DEV bool tok_put(TokOut &to, uint32_t t, uint8_t *pool) {
-  to.t0 = to.t1;
-  to.t1 = to.t2;
-  to.t2 = to.t3;
-  to.t3 = t;
-  if (++to.n < 4) return true;
+  to.t0 = __builtin_amdgcn_alignbit(to.t1, to.t0, 16);
+  to.t1 = __builtin_amdgcn_alignbit(to.t2, to.t1, 16);
+  to.t2 = __builtin_amdgcn_alignbit(to.t3, to.t2, 16);
+  to.t3 = __builtin_amdgcn_alignbit(t, to.t3, 16);
+  if (++to.n < 8) return true;
   bool ok = true;
   if (to.pend) ok = tok_store(to, to.p0, to.p1, to.p2, to.p3, pool);
   to.p0 = to.t0;
@@ -248,19 +242,6 @@ SB_DEV bool tok_put(TokOut &to, uint32_t t, uint8_t *pool) {
   to.pend = true;
   to.n = 0;
   return ok;
-}
-SB_DEV bool tok_close_lits(TokOut &to, uint8_t *pool) {
-  if (!to.pc) return true;
-  const uint32_t w = to.pw | (to.pc << 24);
-  to.pw = to.pc = 0;
-  return tok_put(to, w, pool);
-}
-SB_DEV bool tok_lit(TokOut &to, uint32_t byte, uint8_t *pool) {
-  to.pw |= byte << (8 * to.pc);
-  return ++to.pc < 3 ? true : tok_close_lits(to, pool);
-}
-SB_DEV bool tok_put_match(TokOut &to, uint32_t len, uint32_t dist, uint8_t *pool) {
-  return tok_close_lits(to, pool) && tok_put(to, tok_match(len, dist), pool);
 }
 
 enum : int { S_NEXT = 0, S_HDR = 1, S_HUFF = 2, S_STORED = 3, S_DONE = 4, S_EXIT = 5, S_PARK = 6 };
@@ -314,7 +295,7 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
   for (int k = 0; k < 16; k++) A[k] = 0;
 #pragma unroll
   for (int k = 0; k < 8; k++) B[k] = 0;
-  TokOut to{0, 0, 0, 0, 0, 0, 0, 0, 0, false, 0, 0, 0};
+  TokOut to{0, 0, 0, 0, 0, 0, 0, 0, 0, false, 0};
   Canon lc, dc;
   int32_t o = 0, us = 0, err = INF_OK, sleft = 0, fin = 0;
   auto refill = [&]() {  // the symbol loop's refill: next dword from the register window
@@ -350,7 +331,6 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
             to.cur = tok_region(bt.uoff[blk], blk);
             to.n = 0;
             to.pend = false;
-            to.pw = to.pc = 0;
             // word pointer derived from d by arithmetic only (an integer round trip would make it a flat
             // pointer, whose loads the compiler must wait for together with every LDS access)
             const int64_t a = st + hs;
@@ -601,7 +581,7 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
         int len = 0;
         bool is_len = false;
         if (sym < 256) {
-          if (!tok_lit(to, (uint32_t)sym, pool)) err = INF_OVERFLOW;
+          if (!tok_put(to, (uint32_t)sym, pool)) err = INF_OVERFLOW;
           o++;
           if (o == us || err != INF_OK) state = S_DONE;
         } else if (sym == 256) {
@@ -635,7 +615,7 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
           if (!is_len) {
             if (v2 && i2 < h2 && br.left >= L2) {
               br.drop(L2);
-              if (!tok_lit(to, (uint32_t)b2, pool)) err = INF_OVERFLOW;
+              if (!tok_put(to, (uint32_t)b2, pool)) err = INF_OVERFLOW;
               o++;
               if (o == us || err != INF_OK) state = S_DONE;
             }
@@ -661,7 +641,10 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
                   err = INF_DATA;  // invalid distance too far back
                   state = S_DONE;
                 } else {
-                  if (!tok_put_match(to, (uint32_t)len, (uint32_t)dist, pool)) err = INF_OVERFLOW;
+                  bool ok = true;
+                  ok = ok && tok_put(to, (uint32_t)(len + 253), pool);
+                  ok = ok && tok_put(to, kTokDist | (uint32_t)(dist - 1), pool);
+                  if (!ok) err = INF_OVERFLOW;
                   o = min(o + len, us);
                   if (o == us || err != INF_OK) state = S_DONE;
                 }
@@ -677,7 +660,7 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
       int m = 0;
       for (int i = 0; i < 2; i++) {
         if (i < n && br.left >= 8 && err == INF_OK) {
-          if (!tok_lit(to, br.peek(8), pool)) err = INF_OVERFLOW;
+          if (!tok_put(to, br.peek(8), pool)) err = INF_OVERFLOW;
           br.drop(8);
           m++;
         }
@@ -700,16 +683,15 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
       }
     }
     if (state == S_DONE) {
-      if (err != INF_OVERFLOW) {  // the open literal word, the final chunk (padded with empty words) and any
-        bool ok = tok_close_lits(to, pool);  // pending one leave now
+      if (err != INF_OVERFLOW) {  // final (padded) chunk and any pending one leave now
+        bool ok = true;
         if (to.n > 0)
-          while (ok && to.n > 0) ok = tok_put(to, 0u, pool);
+          while (ok && to.n > 0) ok = tok_put(to, kTokPad, pool);
         if (ok && to.pend) ok = tok_store(to, to.p0, to.p1, to.p2, to.p3, pool);
         if (!ok) err = INF_OVERFLOW;
       }
       to.n = 0;
       to.pend = false;
-      to.pw = to.pc = 0;
       status[blk] = err;
       found[blk] = err == INF_OVERFLOW ? 0 : o;  // an overflowed block has no complete token stream
       state = S_NEXT;
@@ -817,16 +799,6 @@ SB_DEV uint32_t wave_incl_scan(uint32_t x) {
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
   x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
   return x;
-}
-
-// Literal words of the wave decoder (k_inflate_wave): a literal opens a new word unless the open word holds 1 or
-// 2 literals and the previous literal started in the same input dword.  The rule depends only on input positions,
-// so two decodes of one stream that meet at a symbol boundary agree on the words from the next literal that
-// starts a dword on (or the next match) — what phase B's checkpoints need; lit_key is the part of the state that
-// decides the next word there (0: the next literal opens one).
-SB_DEV bool lit_opens(uint32_t pc, uint32_t pq, uint32_t p0) { return pc == 0u || pc == 3u || (p0 >> 5) != pq; }
-SB_DEV uint32_t lit_key(uint32_t pc, uint32_t pq, uint32_t rp) {
-  return (pc == 1u || pc == 2u) && (rp >> 5) == pq ? pc : 0u;
 }
 
 // Decode table of one alphabet from lens[off, off + nsym), by the whole wave, into tab[toff, ...).  Returns false
@@ -1199,8 +1171,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       {
         int stt = lane == 0 ? (int)((S >> 9) & 1) : 0;
         uint32_t pl = lane == 0 ? (S & 511u) : 0u;
-        uint32_t pc = 0, pq = 0;  // open literal word: literals in it, input dword of the last one (lit_opens)
-        int rp = seg_start;       // reader position
+        int rp = seg_start;  // reader position
         bool go = true;
         if (seg_start >= pend && lane > 0) {
           go = false;
@@ -1227,23 +1198,18 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
             nst++;
             go = !outp;
           }
-          // words: a literal that opens one (lit_opens), a distance (its match word)
-          const bool lit = !stp && kind == K_LIT;
-          const bool nw = lit && lit_opens(pc, pq, p0);
-          tokA += (nw || (!stp && kind == K_DIST)) ? 1u : 0u;
+          tokA += stp ? 0u : 1u;
           bytA += stp ? 0u : kind == K_LIT ? 1u : kind == K_LEN ? v : 0u;
-          pc = stp ? pc : lit ? (nw ? 1u : pc + 1u) : 0u;
-          pq = lit ? p0 >> 5 : pq;
           pl = (!stp && kind == K_LEN) ? v : pl;
           stt = (!stp && kind == K_LEN) ? 1 : 0;
         };
         // checkpoints every kCpSteps steps (wave-uniform, so a record costs no divergent branch): the lane's
-        // position if it is at a literal/length boundary, its counts and its literal-word key there
+        // position if it is at a literal/length boundary
         sfor<0, kCp>([&](auto J) {
           constexpr int jj = decltype(J)::value;
           const bool live = go && rp < seg_end;
           cp[jj] = (live && stt == 0) ? (uint32_t)rp : ~0u;
-          cc[jj] = tokA | (bytA << 12) | (lit_key(pc, pq, (uint32_t)rp) << 29);
+          cc[jj] = tokA | (bytA << 12);
 #pragma unroll 1
           for (int k = 0; k < kCpSteps; k++)
             if (go && rp < seg_end) step();
@@ -1278,7 +1244,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         WADD(7, 1);
         if (need) {
           int stt = (int)((pex >> 9) & 1);
-          uint32_t pl = pex & 511u, tk = 0, by = 0, pc = 0, pq = 0;
+          uint32_t pl = pex & 511u, tk = 0, by = 0;
           int rp = (int)(pex >> 10);
           // the first checkpoint at or after the reader
           auto next_cp = [&](uint32_t p) {
@@ -1291,13 +1257,9 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
           };
           uint32_t tcp = next_cp((uint32_t)rp);
           for (;;) {
-            uint32_t cj = 0;
-            if (stt == 0 && (uint32_t)rp == tcp) {
+            if (stt == 0 && (uint32_t)rp == tcp) {  // on the first-pass path from here
+              uint32_t cj = 0;
               sfor<0, kCp>([&](auto I) { cj = cp[decltype(I)::value] == tcp ? cc[decltype(I)::value] : cj; });
-            }
-            if (stt == 0 && (uint32_t)rp == tcp && (cj >> 29) == lit_key(pc, pq, (uint32_t)rp)) {
-              // on the first-pass path from here, with the same open literal word: the counts from here on agree
-              cj &= (1u << 29) - 1u;
               const uint32_t P = tcp;
               // the first recorded stop at or after the checkpoint ends the path
               const bool h1 = nst >= 1 && s1p >= P, h2 = !h1 && nst >= 2 && s2p >= P;
@@ -1318,18 +1280,14 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
               break;
             }
             uint32_t v;
-            const uint32_t p0 = (uint32_t)rp;
             const uint32_t kind = (wsym(L, wq, rp, stt, v) >> 8) & 3u;
             const bool outp = rp > pend;
             if (kind == K_SPEC || outp) {
               res = SegResult{tk, by, (uint32_t)rp << 10, outp ? ST_OUT : v == 0 ? ST_EOB : ST_ERR, false};
               break;
             }
-            const bool nw = kind == K_LIT && lit_opens(pc, pq, p0);
-            tk += (nw || kind == K_DIST) ? 1u : 0u;
+            tk++;
             by += kind == K_LIT ? 1u : kind == K_LEN ? v : 0u;
-            pc = kind == K_LIT ? (nw ? 1u : pc + 1u) : 0u;
-            pq = kind == K_LIT ? p0 >> 5 : pq;
             pl = kind == K_LEN ? v : pl;
             stt = kind == K_LEN ? 1 : 0;
             if ((uint32_t)rp > tcp) tcp = next_cp((uint32_t)rp);
@@ -1346,8 +1304,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       const uint32_t itok = wave_incl_scan(my_tok), ibyt = wave_incl_scan(my_byt);
       const uint32_t tot_tok = uni((uint32_t)__shfl(itok, 63)), tot_byt = uni((uint32_t)__shfl(ibyt, 63));
       const int stop_f = f < 64 ? uni(__shfl(res.stop, f)) : ST_NONE;
-      if (stop_f == ST_ERR || stop_f == ST_OUT || out + (int)tot_byt > us || __ballot(act && res.bad) != 0 ||
-          4 * (ntok + (int)tot_tok) > 2 * us + 32) {  // (words past the region: only a pathological stream)
+      if (stop_f == ST_ERR || stop_f == ST_OUT || out + (int)tot_byt > us || __ballot(act && res.bad) != 0) {
         ok = false;
         break;
       }
@@ -1361,27 +1318,18 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         int rp = (int)(start >> 10);
         int o = out + (int)(ibyt - my_byt);
         uint32_t ti = (uint32_t)ntok + (itok - my_tok);
-        uint32_t pw = 0, pc = 0, pq = 0;  // open literal word
-        uint32_t *rw = reinterpret_cast<uint32_t *>(reg);
         while (rp < seg_end) {
           uint32_t v;
-          const uint32_t p0 = (uint32_t)rp;
           const uint32_t kind = (wsym(L, wq, rp, stt, v) >> 8) & 3u;
           if (kind == K_SPEC) break;  // the end-of-block symbol of lane f
-          // at most one word leaves per symbol: the open literal word when this symbol closes it (a literal that
-          // opens a new word, or a length), or the match word at its distance
-          const bool lit = kind == K_LIT, dist = kind == K_DIST;
-          const bool nw = lit && lit_opens(pc, pq, p0);
-          if ((pc != 0u && (nw || !lit)) || dist) rw[ti++] = dist ? tok_match(pl, v) : pw | (pc << 24);
-          derr |= dist && (int)v > o - (int)pl;
-          pw = lit ? (nw ? v : pw | (v << (8 * pc))) : 0u;
-          pc = lit ? (nw ? 1u : pc + 1u) : 0u;
-          pq = lit ? p0 >> 5 : pq;
+          const uint32_t t = kind == K_LIT ? v : kind == K_LEN ? v + 253u : kTokDist | (v - 1u);
+          if (kind == K_DIST) derr |= (int)v > o - (int)pl;
           o += kind == K_LIT ? 1 : kind == K_LEN ? (int)v : 0;
           pl = kind == K_LEN ? v : pl;
           stt = kind == K_LEN ? 1 : 0;
+          *reinterpret_cast<uint16_t *>(reg + 2 * ti) = (uint16_t)t;
+          ti++;
         }
-        if (pc) rw[ti] = pw | (pc << 24);
       }
       WMARK(5);
       if (__ballot(derr) != 0) { ok = false; break; }
@@ -1479,55 +1427,65 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
   const int64_t U0 = bt.uoff[b];
   uint8_t *ob = out + U0;
   const uint32_t Gr = (uint32_t)U0 & G::kMask;  // ring byte of position 0
-  const uint32_t *wp = reinterpret_cast<const uint32_t *>(pool + tok_region(U0, b));
+  const uint16_t *tk = reinterpret_cast<const uint16_t *>(pool + tok_region(U0, b));
   const int F0 = (int)((16 - (U0 & 15)) & 15);  // first position on a 16-B boundary
   int F = F0;                                     // flushed up to here (from F0)
   bool head = F0 == 0;                            // positions [0, F0) stored
   int Z = -(int)(Gr & 3u);                        // ring zeroed for positions [.., Z); Gr + Z is dword aligned
-  int B = 0, wi = 0;
-  uint32_t w = wp[lane];
+  int B = 0, tp = 0;                              // chunk base position, its first token
+  // lane i holds tokens tp + 2i and tp + 2i + 1, and sees tp + 2i + 2 (the distance of a length in its second)
+  uint32_t ta = tk[2 * lane], tb = tk[2 * lane + 1], tn = tk[2 * lane + 2];
   while (B < ae) {
-    // ---- 1. positions
-    const bool isM = (int32_t)w < 0;
-    const int Lw = isM ? (int)((w >> 16) & 255u) + 3 : (int)((w >> 24) & 3u);
-    const int incl = (int)wave_incl_scan((uint32_t)Lw);
-    const int ex = incl - Lw;
+    // ---- 1. positions: a lane yields up to 2 literals and at most one match (a length in its first token takes
+    // the second as its distance; a length in its second takes the next lane's first)
+    const bool aLit = ta < 256u, aLen = (ta >> 8) == 1u, bLit = tb < 256u, bLen = (tb >> 8) == 1u;
+    const int nl = (int)aLit + (int)bLit;
+    const int Lm = aLen ? (int)ta - 253 : bLen ? (int)tb - 253 : 0;
+    const int d = (int)((aLen ? tb : tn) & 0x7fffu) + 1;
+    const int Ln = nl + Lm;
+    const int incl = (int)wave_incl_scan((uint32_t)Ln);
+    const int ex = incl - Ln;
     const int O = B + ex;
     const bool take = ex < rs::kSpan && O < ae;
-    const int nt = __popcll(__ballot(take));  // a prefix of the lanes (lane 0 always)
+    const uint64_t tmask = __ballot(take);
+    const int nt = __popcll(tmask);  // a prefix of the lanes (lane 0 always)
     const int E = min(B + __builtin_amdgcn_readlane(incl, nt - 1), ae);
-    const int wi2 = uni(wi + nt);
-    const uint32_t wn = wp[wi2 + lane];  // next chunk's words (reads past the stream stay inside the pool)
+    if (E <= B) break;  // (no output left in the tokens: never for a decoded stream)
+    // the next chunk starts after the last taken lane's tokens (and the distance its second token may own)
+    const int tp2 = uni(tp + 2 * nt + (int)((__ballot(bLen) >> (nt - 1)) & 1ull));
+    const uint32_t ta2 = tk[tp2 + 2 * lane], tb2 = tk[tp2 + 2 * lane + 1], tn2 = tk[tp2 + 2 * lane + 2];
     // ---- 2. zero the ring dwords of [Z, E)
     {
       const uint32_t z0 = (Gr + (uint32_t)Z) >> 2, z1 = (Gr + (uint32_t)E + 3u) >> 2;
       for (uint32_t k = z0 + (uint32_t)lane; k < z1; k += 64u) ring[k & G::kDwMask] = 0u;
       Z = (int)(z1 * 4u - Gr);
     }
-    const int Le = take ? min(Lw, ae - O) : 0;
-    // ---- 3a. literal words
-    if (take && !isM && Le > 0) {
-      const uint32_t v = w & (Le >= 3 ? 0xffffffu : Le == 2 ? 0xffffu : 0xffu);
+    // ---- 3a. literals (before the match when a lane has both)
+    const int Ll = take ? min(nl, ae - O) : 0;
+    if (Ll > 0) {
+      const uint32_t lv = aLit ? (ta | (bLit ? tb << 8 : 0u)) : tb;
+      const uint32_t v = lv & (Ll >= 2 ? 0xffffu : 0xffu);
       const uint32_t x = (Gr + (uint32_t)O) & G::kMask, q = x >> 2, s8 = (x & 3u) * 8u;
       const uint64_t sv = (uint64_t)v << s8;
       atomicOr(ring + q, (uint32_t)sv);
       if ((uint32_t)(sv >> 32)) atomicOr(ring + ((q + 1u) & G::kDwMask), (uint32_t)(sv >> 32));
     }
     // ---- 3b. matches, in rounds
-    const int d = (int)(w & 0x7fffu) + 1;
-    const bool mt = take && isM && Le > 0;
+    const int mO = O + (bLen ? nl : 0);
+    const int Le = (take && Lm > 0) ? min(Lm, ae - mO) : 0;
+    const bool mt = Le > 0;
     const bool far = d > G::kNear;
-    const int srcEnd = O - d + min(Le, d);
+    const int srcEnd = mO - d + min(Le, d);
     uint64_t pend = __ballot(mt);
     while (pend) {
       const int f = __ffsll((unsigned long long)pend) - 1;
-      const int fr = __builtin_amdgcn_readlane(O, f);
+      const int fr = __builtin_amdgcn_readlane(mO, f);
       const uint64_t ready = pend & __ballot(srcEnd <= fr);
       if ((ready >> lane) & 1ull) {
         int done = 0, deff = d;
         while (done < Le) {
           const int n = min(min(Le - done, 16), deff);
-          const int src = O + done - deff;
+          const int src = mO + done - deff;
           uint32_t v0, v1, v2, v3;
           if (far) {  // below the flushed mark: one unaligned 16-B load, past this CU's L1 (nt)
             const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(ob + src));
@@ -1559,7 +1517,7 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
           v2 &= (uint32_t)mhi;
           v3 &= (uint32_t)(mhi >> 32);
           // shift to the destination's byte offset and OR in
-          const uint32_t xd = (Gr + (uint32_t)(O + done)) & G::kMask, qd = xd >> 2, s8 = (xd & 3u) * 8u;
+          const uint32_t xd = (Gr + (uint32_t)(mO + done)) & G::kMask, qd = xd >> 2, s8 = (xd & 3u) * 8u;
           const uint64_t a01 = ((uint64_t)v1 << 32 | v0) << s8, a12 = ((uint64_t)v2 << 32 | v1) << s8,
                          a23 = ((uint64_t)v3 << 32 | v2) << s8, a34 = (uint64_t)v3 << s8;
           ring_or5<G>(ring, qd, (uint32_t)a01, (uint32_t)(a01 >> 32), (uint32_t)(a12 >> 32), (uint32_t)(a23 >> 32),
@@ -1581,8 +1539,10 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
       *reinterpret_cast<uint4 *>(ob + F + 16 * lane) = *reinterpret_cast<const uint4 *>(ring8 + x);
       F += rs::kFlush;
     }
-    w = wn;
-    wi = wi2;
+    ta = ta2;
+    tb = tb2;
+    tn = tn2;
+    tp = tp2;
   }
   // tail: the head (a block shorter than its first partial chunk), whole 16-B chunks, the last partial chunk
   if (!head) {
