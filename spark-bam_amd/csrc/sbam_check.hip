@@ -22,8 +22,15 @@
 #include "sbam_internal.h"
 
 // k_check workgroups per CU the register budget is sized for (launch bounds): boundary tiles / interior tiles
+#ifndef SBAM_CHECK_WGS
 #define SBAM_CHECK_WGS 4
+#endif
+#ifndef SBAM_CHECK_WGS_INT
 #define SBAM_CHECK_WGS_INT 5
+#endif
+#ifndef SBAM_LDS_LENS
+#define SBAM_LDS_LENS 4096
+#endif
 
 namespace sbam {
 
@@ -38,7 +45,7 @@ constexpr int kHalo = 768;                  // staged bytes past the tile (fixed
 constexpr int kWin = kTile + kHalo;         // staged window (multiple of 16)
 constexpr int kOpcWords = kWin / 128 + 4;   // per residue class: one bit per 4 window bytes (+ pad)
 constexpr int kNameWords = kWin / 32 + 4;   // one bit per window byte (+ pad)
-constexpr int kLdsLens = 4096;              // contig lengths kept in LDS when n_ref fits
+constexpr int kLdsLens = SBAM_LDS_LENS;     // contig lengths kept in LDS when n_ref fits
 constexpr int kFlushTiles = 7;              // 7 tiles x 32 positions per lane < 255 (8-bit planes / counters)
 static_assert(kWin % 16 == 0, "window");
 
@@ -592,6 +599,39 @@ SB_DEV uint32_t check_first(const Tile &t, const StreamView &sv, const int32_t *
   return w;
 }
 
+// check_first<false, true> without its rare tails, branch-free: a name body or an op array longer than the 64
+// bytes / ops one bitmap read covers sets `rare` (the caller redoes that position with check_first).  Returns the
+// flag word F (0: record 0 passed).  With no branch inside, the four positions of a lane form one basic block
+// that the scheduler can interleave (a compare → select chain per position otherwise waits on its own VCC).
+SB_DEV uint32_t check_first_int(const Tile &t, const int32_t *lensL, int32_t nref, int rel, const int32_t f[8],
+                                bool &rare) {
+  const int32_t bs = f[0], ri = f[1], rp = f[2], bmn = f[3], fnc = f[4], ls = f[5], nri = f[6], nrp = f[7];
+  const int32_t lrn = bmn & 0xff;
+  const uint32_t flag = ((uint32_t)fnc) >> 16;
+  const int32_t nc = fnc & 0xffff;
+  const uint32_t rb0 = ref_bits_lds(ri, rp, lensL, nref), rb1 = ref_bits_lds(nri, nrp, lensL, nref);
+  const bool empty_mapped = (flag & 4u) == 0 && (ls == 0 || nc == 0);
+  const bool has_name = lrn >= 2;
+  const uint32_t last = t.win[rel + 35 + (has_name ? lrn : 1)];
+  const bool scan = has_name && last == 0;
+  const int32_t nbody = lrn - 1;
+  uint64_t nbm = bits64(t.nbad, rel + 36);
+  nbm &= nbody >= 64 ? ~0ull : (1ull << (nbody > 0 ? nbody : 0)) - 1ull;
+  const int crel = rel + 36 + (has_name ? lrn : 0);
+  const uint64_t om = bits64(t.opc + (crel & 3) * kOpcWords, crel >> 2);
+  const int32_t bad = om ? (int32_t)__builtin_ctzll(om) : 64;
+  const bool inv_op = nc > 0 && bad < nc;
+  rare = (scan && nbm == 0 && nbody > 64) || (om == 0 && nc > 64);
+  uint32_t F = (rb0 << 1) | (rb1 << 5) | (too_few_remaining(bs, lrn, nc, ls) ? (1u << 18) : 0u);
+  F |= lrn == 0 ? (1u << 12) : 0u;
+  F |= lrn == 1 ? (1u << 13) : 0u;
+  F |= (has_name && last != 0) ? (1u << 10) : 0u;
+  F |= (scan && nbm != 0) ? (1u << 11) : 0u;
+  F |= inv_op ? (1u << 15) : 0u;
+  F |= (empty_mapped && !inv_op) ? (((ls == 0) ? (1u << 16) : 0u) | ((nc == 0) ? (1u << 17) : 0u)) : 0u;
+  return F;
+}
+
 // Stage the window of the tile at `base` (32 B per lane per step) and build the op-class and name-character
 // bitmaps (struct Tile).
 SB_DEV void stage_tile(const StreamView &sv, int64_t base, uint8_t *s_win, uint32_t *s_opc, uint32_t *s_nbad) {
@@ -825,15 +865,44 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
 #pragma unroll
       for (int q = 0; q < 10; q++) W[q] = w32[g + q];
       uint32_t wd[4];
+      if constexpr (INTERIOR && MODE == MODE_COUNTS) {
+        // branch-free record-0 checks of the 4 positions, then one wave-uniform fix-up for the rare long tails
+        bool rr[4];
 #pragma unroll
-      for (int o = 0; o < 4; o++) {
-        const int64_t x = xg + o;
-        int32_t f[8];
+        for (int o = 0; o < 4; o++) {
+          int32_t f[8];
 #pragma unroll
-        for (int q = 0; q < 8; q++) f[q] = (int32_t)__builtin_amdgcn_alignbyte(W[q + 1], W[q], o);
-        uint32_t w = check_first<EAGER, INTERIOR>(tl, sv, lensL, x, 4 * g + o, R, f);
-        if (!INTERIOR) w = (x >= x0 && x < x1) ? w : W_NONE;  // interior tiles lie inside [x0, x1)
-        wd[o] = w;
+          for (int q = 0; q < 8; q++) f[q] = (int32_t)__builtin_amdgcn_alignbyte(W[q + 1], W[q], o);
+          const uint32_t F = check_first_int(tl, lensL, sv.nref, 4 * g + o, f, rr[o]);
+          wd[o] = (F && R > 0) ? F : W_PASS0;
+        }
+        const uint32_t rm = (rr[0] ? 1u : 0u) | (rr[1] ? 2u : 0u) | (rr[2] ? 4u : 0u) | (rr[3] ? 8u : 0u);
+        if (__ballot(rm != 0u)) {  // (one copy of the exact path, looped: it must not cost registers)
+#pragma unroll 1
+          for (int o = 0; o < 4; o++) {
+            if ((rm >> o) & 1u) {
+              int32_t f[8];
+#pragma unroll
+              for (int q = 0; q < 8; q++) f[q] = (int32_t)__builtin_amdgcn_alignbyte(W[q + 1], W[q], (uint32_t)o);
+              const uint32_t w = check_first<false, true>(tl, sv, lensL, xg + o, 4 * g + o, R, f);
+              wd[0] = o == 0 ? w : wd[0];
+              wd[1] = o == 1 ? w : wd[1];
+              wd[2] = o == 2 ? w : wd[2];
+              wd[3] = o == 3 ? w : wd[3];
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int o = 0; o < 4; o++) {
+          const int64_t x = xg + o;
+          int32_t f[8];
+#pragma unroll
+          for (int q = 0; q < 8; q++) f[q] = (int32_t)__builtin_amdgcn_alignbyte(W[q + 1], W[q], o);
+          uint32_t w = check_first<EAGER, INTERIOR>(tl, sv, lensL, x, 4 * g + o, R, f);
+          if (!INTERIOR) w = (x >= x0 && x < x1) ? w : W_NONE;  // interior tiles lie inside [x0, x1)
+          wd[o] = w;
+        }
       }
       if (MODE == MODE_WORDS) {
 #pragma unroll
@@ -849,13 +918,29 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
       v |= shfl_xor64(v, 2);
       v |= shfl_xor64(v, 4);
       v |= shfl_xor64(v, 8);
-      if ((lane & 15) == 0 && (INTERIOR || xg < x1)) bitmap[(xg - x0a) >> 6] = v;  // word holds >= 1 position < x1
+      if (INTERIOR) {
+        bitmap[(xg - x0a) >> 6] = v;  // the 16 lanes of a word store the same value: no branch
+      } else if ((lane & 15) == 0 && xg < x1) {
+        bitmap[(xg - x0a) >> 6] = v;  // word holds >= 1 position < x1
+      }
       if (!COUNTS) continue;
       uint32_t Fo[4];
       if constexpr (INTERIOR && !BYKEY) {
         uint32_t oh[4];
+        bool low = false;
 #pragma unroll
-        for (int o = 0; o < 4; o++) Fo[o] = classify_interior(wd[o], s_k12, s_pair, oh[o]);
+        for (int o = 0; o < 4; o++) {
+          Fo[o] = wd[o] & 0x7ffffu;
+          oh[o] = 1u << __popc(Fo[o]);
+          low |= (oh[o] & 6u) != 0;  // key 1 or 2
+        }
+        if (__ballot(low)) {
+#pragma unroll
+          for (int o = 0; o < 4; o++) {
+            uint32_t oh2;
+            if (oh[o] & 6u) classify_interior(wd[o], s_k12, s_pair, oh2);
+          }
+        }
         add4(acc.kp, oh);
       } else {
 #pragma unroll

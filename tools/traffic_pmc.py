@@ -21,7 +21,7 @@ from collections import defaultdict
 KERNELS = {"k_check<0, 1>": "sbam::k_check<0, 1>", "k_check<0, 2>": "sbam::k_check<0, 2>",
            "k_p0_links": "sbam::k_p0_links", "k_p0_list": "sbam::k_p0_list", "k_p0_count": "sbam::k_p0_count",
            "k_inflate_decode": "sbam::k_inflate_wave", "k_inflate_slow": "sbam::k_inflate_slow",
-           "k_inflate_resolve": "sbam::k_inflate_resolve", "k_check<1, 0>": "sbam::k_check<1, 0>",
+           "k_inflate_resolve": "sbam::k_inflate_resolve<12>", "k_check<1, 0>": "sbam::k_check<1, 0>",
            "k_check<1, 1>": "sbam::k_check<1, 1>", "k_check<1, 2>": "sbam::k_check<1, 2>",
            "k_chains": "sbam::k_chains",
            "k_scan_count": "sbam::k_scan_count", "k_scan_write": "sbam::k_scan_write",
