@@ -604,7 +604,7 @@ SB_DEV uint32_t check_first(const Tile &t, const StreamView &sv, const int32_t *
 // flag word F (0: record 0 passed).  With no branch inside, the four positions of a lane form one basic block
 // that the scheduler can interleave (a compare → select chain per position otherwise waits on its own VCC).
 SB_DEV uint32_t check_first_int(const Tile &t, const int32_t *lensL, int32_t nref, int rel, const int32_t f[8],
-                                bool &rare) {
+                                const uint64_t *lomask, uint64_t nbm, bool &rare) {
   const int32_t bs = f[0], ri = f[1], rp = f[2], bmn = f[3], fnc = f[4], ls = f[5], nri = f[6], nrp = f[7];
   const int32_t lrn = bmn & 0xff;
   const uint32_t flag = ((uint32_t)fnc) >> 16;
@@ -612,15 +612,13 @@ SB_DEV uint32_t check_first_int(const Tile &t, const int32_t *lensL, int32_t nre
   const uint32_t rb0 = ref_bits_lds(ri, rp, lensL, nref), rb1 = ref_bits_lds(nri, nrp, lensL, nref);
   const bool empty_mapped = (flag & 4u) == 0 && (ls == 0 || nc == 0);
   const bool has_name = lrn >= 2;
-  const uint32_t last = t.win[rel + 35 + (has_name ? lrn : 1)];
+  const uint32_t last = t.win[rel + 35 + lrn];  // (read for lrn < 2 too, unused then)
   const bool scan = has_name && last == 0;
   const int32_t nbody = lrn - 1;
-  uint64_t nbm = bits64(t.nbad, rel + 36);
-  nbm &= nbody >= 64 ? ~0ull : (1ull << (nbody > 0 ? nbody : 0)) - 1ull;
+  nbm &= lomask[nbody < 0 ? 0 : nbody > 64 ? 64 : nbody];  // lomask[n]: the low n bits
   const int crel = rel + 36 + (has_name ? lrn : 0);
   const uint64_t om = bits64(t.opc + (crel & 3) * kOpcWords, crel >> 2);
-  const int32_t bad = om ? (int32_t)__builtin_ctzll(om) : 64;
-  const bool inv_op = nc > 0 && bad < nc;
+  const bool inv_op = (om & lomask[nc > 64 ? 64 : nc]) != 0;  // an invalid op among the first min(nc, 64)
   rare = (scan && nbm == 0 && nbody > 64) || (om == 0 && nc > 64);
   uint32_t F = (rb0 << 1) | (rb1 << 5) | (too_few_remaining(bs, lrn, nc, ls) ? (1u << 18) : 0u);
   F |= lrn == 0 ? (1u << 12) : 0u;
@@ -827,7 +825,9 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
   __shared__ uint32_t s_cnt[BYKEY ? 21 * 19 : 1];
   __shared__ uint32_t s_k12[3 * 19];    // keys 0-2 × flag (non-BYKEY modes)
   __shared__ uint32_t s_pair[19 * 19];  // close-call pairs (key 2)
+  __shared__ uint64_t s_lomask[65];     // s_lomask[n] = the low n bits
   const int lane = lane_id();
+  for (int i = threadIdx.x; i < 65; i += kCheckThreads) s_lomask[i] = i >= 64 ? ~0ull : (1ull << i) - 1ull;
   for (int i = threadIdx.x; i < 3 * 19; i += kCheckThreads) s_k12[i] = 0;
   for (int i = threadIdx.x; i < 19 * 19; i += kCheckThreads) s_pair[i] = 0;
   const int32_t *lensL = nullptr;
@@ -868,12 +868,19 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
       if constexpr (INTERIOR && MODE == MODE_COUNTS) {
         // branch-free record-0 checks of the 4 positions, then one wave-uniform fix-up for the rare long tails
         bool rr[4];
+        // the name-character bitmap from bit 4g + 36 on, read once for the 4 positions (bits 4g + 36 + o ..)
+        const int nb0 = 4 * g + 36, nw = nb0 >> 5;
+        const uint32_t n0 = s_nbad[nw], n1 = s_nbad[nw + 1], n2 = s_nbad[nw + 2], n3 = s_nbad[nw + 3];
 #pragma unroll
         for (int o = 0; o < 4; o++) {
           int32_t f[8];
 #pragma unroll
           for (int q = 0; q < 8; q++) f[q] = (int32_t)__builtin_amdgcn_alignbyte(W[q + 1], W[q], o);
-          const uint32_t F = check_first_int(tl, lensL, sv.nref, 4 * g + o, f, rr[o]);
+          const uint32_t sb = (uint32_t)(nb0 + o) & 31u;  // bit offset in n0.. (the +o may carry into n1)
+          const bool up = (nb0 & 31) + o >= 32;
+          const uint32_t a0 = up ? n1 : n0, a1 = up ? n2 : n1, a2 = up ? n3 : n2;
+          const uint64_t nbm = ((uint64_t)__builtin_amdgcn_alignbit(a2, a1, sb) << 32) | __builtin_amdgcn_alignbit(a1, a0, sb);
+          const uint32_t F = check_first_int(tl, lensL, sv.nref, 4 * g + o, f, s_lomask, nbm, rr[o]);
           wd[o] = (F && R > 0) ? F : W_PASS0;
         }
         const uint32_t rm = (rr[0] ? 1u : 0u) | (rr[1] ? 2u : 0u) | (rr[2] ? 4u : 0u) | (rr[3] ? 8u : 0u);
@@ -913,11 +920,14 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
       uint32_t nib = 0;
 #pragma unroll
       for (int o = 0; o < 4; o++) nib |= (wd[o] == W_PASS0) ? (1u << o) : 0u;
-      uint64_t v = (uint64_t)nib << (4 * (lane & 15));
-      v |= shfl_xor64(v, 1);
-      v |= shfl_xor64(v, 2);
-      v |= shfl_xor64(v, 4);
-      v |= shfl_xor64(v, 8);
+      uint64_t v = 0;
+      if (__ballot(nib != 0u)) {  // (a wave's 256 positions hold no record-0 pass about half the time)
+        v = (uint64_t)nib << (4 * (lane & 15));
+        v |= shfl_xor64(v, 1);
+        v |= shfl_xor64(v, 2);
+        v |= shfl_xor64(v, 4);
+        v |= shfl_xor64(v, 8);
+      }
       if (INTERIOR) {
         bitmap[(xg - x0a) >> 6] = v;  // the 16 lanes of a word store the same value: no branch
       } else if ((lane & 15) == 0 && xg < x1) {
