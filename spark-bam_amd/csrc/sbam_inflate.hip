@@ -1419,8 +1419,13 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
                                                         const int32_t *__restrict__ found) {
   using G = RingGeom<RB>;
   __shared__ __attribute__((aligned(16))) uint32_t ring[G::kDw];
+  __shared__ __attribute__((aligned(16))) uint32_t s_keep[17 * 4];  // s_keep[4n..4n+3]: mask of the low n bytes
   uint8_t *ring8 = reinterpret_cast<uint8_t *>(ring);
   const int lane = (int)threadIdx.x;
+  for (int i = lane; i < 17 * 4; i += 64) {
+    const int n = i >> 2, k = i & 3, nb = n - 4 * k;  // bytes of dword k kept
+    s_keep[i] = nb >= 4 ? ~0u : nb <= 0 ? 0u : (1u << (8 * nb)) - 1u;
+  }
   const int64_t b = blockIdx.x;
   const int ae = found[b];  // output bytes of the block
   if (ae <= 0) return;
@@ -1476,19 +1481,29 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
     const bool mt = Le > 0;
     const bool far = d > G::kNear;
     const int srcEnd = mO - d + min(Le, d);
+    // far sources (already in HBM, final) are loaded now, 32 B ahead; their copies wait until a near copy needs
+    // them (the first pending match is far), so the loads overlap the near rounds
+    u32x4 pf0 = {0u, 0u, 0u, 0u}, pf1 = {0u, 0u, 0u, 0u};
+    if (mt && far) {
+      pf0 = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(ob + mO - d));
+      if (Le > 16) pf1 = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(ob + mO - d + 16));
+    }
+    const uint64_t farm = __ballot(mt && far);
     uint64_t pend = __ballot(mt);
     while (pend) {
       const int f = __ffsll((unsigned long long)pend) - 1;
       const int fr = __builtin_amdgcn_readlane(mO, f);
-      const uint64_t ready = pend & __ballot(srcEnd <= fr);
+      uint64_t ready = pend & __ballot(srcEnd <= fr);
+      if (!((farm >> f) & 1ull)) ready &= ~farm;
       if ((ready >> lane) & 1ull) {
         int done = 0, deff = d;
         while (done < Le) {
           const int n = min(min(Le - done, 16), deff);
           const int src = mO + done - deff;
           uint32_t v0, v1, v2, v3;
-          if (far) {  // below the flushed mark: one unaligned 16-B load, past this CU's L1 (nt)
-            const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(ob + src));
+          if (far) {  // below the flushed mark: unaligned 16-B loads, past this CU's L1 (nt)
+            u32x4 x = done == 0 ? pf0 : pf1;
+            if (done >= 32) x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(ob + src));
             v0 = x.x; v1 = x.y; v2 = x.z; v3 = x.w;
           } else {
             const uint32_t xs = (Gr + (uint32_t)src) & G::kMask, qs = xs >> 2, ss = xs & 3u;
@@ -1509,13 +1524,11 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
             v3 = __builtin_amdgcn_alignbyte(s4, s3, ss);
           }
           // keep the first n bytes
-          const uint32_t nb = (uint32_t)n * 8u;
-          const uint64_t mlo = nb >= 64u ? ~0ull : (1ull << nb) - 1ull;
-          const uint64_t mhi = nb <= 64u ? 0ull : nb >= 128u ? ~0ull : (1ull << (nb - 64u)) - 1ull;
-          v0 &= (uint32_t)mlo;
-          v1 &= (uint32_t)(mlo >> 32);
-          v2 &= (uint32_t)mhi;
-          v3 &= (uint32_t)(mhi >> 32);
+          const uint4 km = *reinterpret_cast<const uint4 *>(s_keep + 4 * n);
+          v0 &= km.x;
+          v1 &= km.y;
+          v2 &= km.z;
+          v3 &= km.w;
           // shift to the destination's byte offset and OR in
           const uint32_t xd = (Gr + (uint32_t)(mO + done)) & G::kMask, qd = xd >> 2, s8 = (xd & 3u) * 8u;
           const uint64_t a01 = ((uint64_t)v1 << 32 | v0) << s8, a12 = ((uint64_t)v2 << 32 | v1) << s8,
