@@ -726,6 +726,12 @@ constexpr int kLitOff = 0, kDistOff = (1 << kLitRoot) + kLitSub;
 constexpr int kTab = kDistOff + (1 << kDistRoot) + kDistSub;
 constexpr int kCp = 12;            // checkpoints per lane
 constexpr int kCpSteps = 8;        // symbols between checkpoints
+// Lanes > 0 start decoding kWarm bits before their segment, so that by the segment start their path has usually
+// resynchronised with the true one: the first symbol boundary at or after the segment start ("entry") then equals
+// the left neighbour's exit and phase A's counts from the entry on need no phase-B re-decode.  Decode at 10 GB:
+// no warm-up 79.5 ms; 128 bits 74.8; 256: 71.6; 384: 69.6; 512 (one segment; lane 1 from the round's true start):
+// 68.5; 640: 70.1; 1024: 76.7.
+constexpr int kWarm = kK;
 constexpr int kScratchDw = 256;    // window tail that doubles as header / table-build scratch
 constexpr uint32_t kSub = 1u << 10;  // table entry flag: pointer to a sub-table
 // a block header (<= 3 + 14 + 57 + 320 * 14 bits) plus the window's start alignment fits before the scratch
@@ -1167,7 +1173,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       });
       uint32_t s1p = ~0u, s1e = 0, s1c = 0, s2p = ~0u, s2e = 0, s2c = 0;  // stops: start, exit | kind, counts
       int nst = 0;
-      uint32_t tokA = 0, bytA = 0, exitEnd;
+      uint32_t tokA = 0, bytA = 0, exitEnd, entry;
       {
         int stt = lane == 0 ? (int)((S >> 9) & 1) : 0;
         uint32_t pl = lane == 0 ? (S & 511u) : 0u;
@@ -1178,7 +1184,21 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
           nst = 1;
           s1p = (uint32_t)seg_start;
           s1e = ((uint32_t)seg_start << 10) | (uint32_t)ST_OUT;
+        } else if (lane > 0 && kWarm > 0) {  // warm-up: decode (uncounted, stops ignored) up to the segment
+          rp = seg_start - kWarm;
+          if (rp <= Sp) {  // from the round's true start, in its true state
+            rp = Sp;
+            stt = (int)((S >> 9) & 1);
+            pl = S & 511u;
+          }
+          while (rp < seg_start) {
+            uint32_t v;
+            const uint32_t kind = (wsym(L, wq, rp, stt, v) >> 8) & 3u;
+            pl = kind == K_LEN ? v : pl;
+            stt = kind == K_LEN ? 1 : 0;
+          }
         }
+        entry = ((uint32_t)rp << 10) | ((uint32_t)stt << 9) | pl;
         auto step = [&]() {
           const uint32_t p0 = (uint32_t)rp;
           uint32_t v;
@@ -1224,7 +1244,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       // ---- phase B: lanes whose true start differs re-decode it until they reach a first-pass checkpoint
       SegResult res = own;
       uint32_t nxt = lane == 0 ? own.exit : exitEnd;  // what the right neighbour starts from (provisional)
-      uint32_t bst = lane == 0 ? S : ((uint32_t)seg_start << 10);
+      uint32_t bst = lane == 0 ? S : entry;
       bool ver = lane == 0;
       int f = 64;
       for (;;) {
