@@ -48,6 +48,7 @@ constexpr int kNameWords = kWin / 32 + 4;   // one bit per window byte (+ pad)
 constexpr int kLdsLens = SBAM_LDS_LENS;     // contig lengths kept in LDS when n_ref fits
 constexpr int kFlushTiles = 7;              // 7 tiles x 32 positions per lane < 255 (8-bit planes / counters)
 static_assert(kWin % 16 == 0, "window");
+static_assert((kTile / (4 * kCheckThreads)) % 2 == 0, "groups pair up within a tile (add4_paired)");
 
 SB_DEV int lane_id() { return __lane_id(); }
 
@@ -756,6 +757,44 @@ SB_DEV uint32_t classify_interior(uint32_t w, uint32_t *k12, uint32_t *pair, uin
   return F;
 }
 
+// Add a 4-plane number (weights 1, 2, 4, 8) into the planes.
+SB_DEV void add_planes4(Planes &pl, uint32_t o1, uint32_t o2, uint32_t o4, uint32_t o8) {
+  uint32_t c = pl.p[0] & o1;
+  pl.p[0] ^= o1;
+  const uint32_t o[3] = {o2, o4, o8};
+#pragma unroll
+  for (int j = 1; j <= 3; j++) {
+    const uint32_t x = pl.p[j] ^ o[j - 1];
+    const uint32_t cn = (pl.p[j] & o[j - 1]) | (c & x);
+    pl.p[j] = x ^ c;
+    c = cn;
+  }
+#pragma unroll
+  for (int j = 4; j < 8; j++) {
+    const uint32_t t = pl.p[j] & c;
+    pl.p[j] ^= c;
+    c = t;
+  }
+}
+// 4:3 compressor of four words into (ones, twos, fours); with a held (ones, twos, fours) from the previous group
+// the two are summed into a 4-plane number and added once (pairs of groups share one carry chain)
+SB_DEV void add4_paired(Planes &pl, const uint32_t v[4], uint32_t (&h)[3], bool second) {
+  const uint32_t x1a = v[0] ^ v[1], c1 = v[0] & v[1];
+  const uint32_t x2a = v[2] ^ v[3], c2 = v[2] & v[3];
+  const uint32_t o1 = x1a ^ x2a, c3 = x1a & x2a;
+  const uint32_t o2 = c1 ^ c2 ^ c3, o4 = (c1 & c2) | (c3 & (c1 ^ c2));
+  if (!second) {
+    h[0] = o1;
+    h[1] = o2;
+    h[2] = o4;
+    return;
+  }
+  const uint32_t s1 = h[0] ^ o1, k1 = h[0] & o1;
+  const uint32_t s2 = h[1] ^ o2 ^ k1, k2 = (h[1] & o2) | (k1 & (h[1] ^ o2));
+  const uint32_t s4 = h[2] ^ o4 ^ k2, k4 = (h[2] & o4) | (k2 & (h[2] ^ o4));
+  add_planes4(pl, s1, s2, s4, k4);
+}
+
 // 4:3 compressor of four bit-plane words into (ones, twos, fours) for Planes::add
 SB_DEV void add4(Planes &pl, const uint32_t v[4]) {
   const uint32_t x1a = v[0] ^ v[1], c1 = v[0] & v[1];
@@ -855,6 +894,7 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
     __syncthreads();
     const Tile tl{s_win, s_opc, s_nbad, base};
     const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
+    uint32_t hkp[3] = {0, 0, 0}, hpl[3] = {0, 0, 0};  // held compressed counts of an even group (add4_paired)
     auto run_tile = [&](auto interior_tag) {
     constexpr bool INTERIOR = decltype(interior_tag)::value;
 #pragma unroll 1
@@ -875,7 +915,7 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
         for (int o = 0; o < 4; o++) {
           int32_t f[8];
 #pragma unroll
-          for (int q = 0; q < 8; q++) f[q] = (int32_t)__builtin_amdgcn_alignbyte(W[q + 1], W[q], o);
+          for (int q = 0; q < 8; q++) f[q] = o == 0 ? (int32_t)W[q] : (int32_t)__builtin_amdgcn_alignbyte(W[q + 1], W[q], o);
           const uint32_t sb = (uint32_t)(nb0 + o) & 31u;  // bit offset in n0.. (the +o may carry into n1)
           const bool up = (nb0 & 31) + o >= 32;
           const uint32_t a0 = up ? n1 : n0, a1 = up ? n2 : n1, a2 = up ? n3 : n2;
@@ -905,7 +945,7 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
           const int64_t x = xg + o;
           int32_t f[8];
 #pragma unroll
-          for (int q = 0; q < 8; q++) f[q] = (int32_t)__builtin_amdgcn_alignbyte(W[q + 1], W[q], o);
+          for (int q = 0; q < 8; q++) f[q] = o == 0 ? (int32_t)W[q] : (int32_t)__builtin_amdgcn_alignbyte(W[q + 1], W[q], o);
           uint32_t w = check_first<EAGER, INTERIOR>(tl, sv, lensL, x, 4 * g + o, R, f);
           if (!INTERIOR) w = (x >= x0 && x < x1) ? w : W_NONE;  // interior tiles lie inside [x0, x1)
           wd[o] = w;
@@ -951,7 +991,7 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
             if (oh[o] & 6u) classify_interior(wd[o], s_k12, s_pair, oh2);
           }
         }
-        add4(acc.kp, oh);
+        add4_paired(acc.kp, oh, hkp, (j & 1) != 0);
       } else {
 #pragma unroll
         for (int o = 0; o < 4; o++) {
@@ -963,7 +1003,8 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
           if (BYKEY) bykey_count(s_cnt, lane, counted, key, Fo[o]);
         }
       }
-      add4(acc.pl, Fo);
+      if constexpr (INTERIOR && !BYKEY) add4_paired(acc.pl, Fo, hpl, (j & 1) != 0);
+      else add4(acc.pl, Fo);
     }
     };
     if constexpr (PART == 1) {
