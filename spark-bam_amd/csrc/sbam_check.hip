@@ -644,17 +644,16 @@ SB_DEV void stage_tile(const StreamView &sv, int64_t base, uint8_t *s_win, uint3
     dst[2 * i] = a;
     dst[2 * i + 1] = b;
     const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    uint32_t cls[4] = {0, 0, 0, 0}, nb = 0;
+    // T: bit j of byte r = byte r of w[j] is an invalid op start, so byte r of T is residue class r's 8 bits
+    uint32_t T = 0, nb = 0;
 #pragma unroll
     for (int j = 0; j < 8; j++) {
-      const uint32_t inv = inv_nibble(w[j]);  // bit r: byte r of w[j] is an invalid op start
-#pragma unroll
-      for (int r = 0; r < 4; r++) cls[r] |= ((inv >> r) & 1u) << j;
-      const uint32_t m = name_bad_bytes(w[j]);  // bit 7 of each bad byte
-      nb |= (((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u)) << (4 * j);
+      T |= ((((w[j] & 0x0f0f0f0fu) + 0x07070707u) >> 4) & 0x01010101u) << j;
+      const uint32_t m = (name_bad_bytes(w[j]) >> 7) & 0x01010101u;  // bit 0 of each bad byte
+      nb |= (((m * 0x00204081u) >> 21) & 0xfu) << (4 * j);
     }
 #pragma unroll
-    for (int r = 0; r < 4; r++) opc8[r * 4 * kOpcWords + i] = (uint8_t)cls[r];
+    for (int r = 0; r < 4; r++) opc8[r * 4 * kOpcWords + i] = (uint8_t)(T >> (8 * r));
     s_nbad[i] = nb;
   }
   if (threadIdx.x < 4) s_nbad[kWin / 32 + threadIdx.x] = 0;
