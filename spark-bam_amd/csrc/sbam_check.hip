@@ -77,11 +77,8 @@ SB_DEV uint32_t wave_or(uint32_t v) {
 }
 
 // ---- byte-class SWAR ---------------------------------------------------------------------------
-// 4 bits: (byte j of w) & 0xf > 8  (Checker.MAX_CIGAR_OP = 8, check/.../check/Checker.scala:21)
-SB_DEV uint32_t inv_nibble(uint32_t w) {
-  const uint32_t t = (((w & 0x0f0f0f0fu) + 0x07070707u) >> 4) & 0x01010101u;
-  return ((t * 0x00204081u) >> 21) & 0xfu;
-}
+// (op validity, Checker.MAX_CIGAR_OP = 8, check/.../check/Checker.scala:21: (b & 0xf) + 7 carries into bit 4 iff
+// (b & 0xf) > 8 — stage_tile)
 // bytes outside allowedReadNameChars = ('!' to '?') ++ ('A' to '~') (Checker.scala:12-17), bit 7 of each byte
 SB_DEV uint32_t name_bad_bytes(uint32_t w) {
   const uint32_t hi = w & 0x80808080u, lo7 = w & 0x7f7f7f7fu;
