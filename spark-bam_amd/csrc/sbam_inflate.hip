@@ -1404,6 +1404,8 @@ constexpr int kFlush = 1024;  // output bytes per group store (64 lanes x 16 B)
 template <int RB>
 struct RingGeom {
   static constexpr uint32_t kRing = 1u << RB, kMask = kRing - 1u, kDw = kRing / 4u, kDwMask = kDw - 1u;
+  // ring dwords [kDw, kDw + kMirror) mirror dwords [0, kMirror): a 5-dword read from any start never wraps
+  static constexpr uint32_t kMirror = 8u;
   // Near sources: the ring holds positions (E + 3 - kRing, E) while a chunk ending at E <= base + kSpan + 257 is
   // written, so every source at distance <= kNear from a word starting before base + kSpan is intact.
   static constexpr int kNear = (int)kRing - rs::kSpan - 264;
@@ -1414,10 +1416,16 @@ struct RingGeom {
   static_assert((int)kRing > rs::kSpan + 260 + rs::kFlush, "slots are flushed before reuse");
 };
 
-// OR up to 5 dwords into the ring at dword q (wrapping).  The common case uses immediate offsets.
+// OR one dword into the ring at (wrapped) dword i, and into its mirror when i < kMirror.
+template <class G>
+SB_DEV void ring_or1(uint32_t *ring, uint32_t i, uint32_t w) {
+  atomicOr(ring + i, w);
+  if (i < G::kMirror) atomicOr(ring + G::kDw + i, w);
+}
+// OR up to 5 dwords into the ring at dword q (wrapping, mirrored).  The common case uses immediate offsets.
 template <class G>
 SB_DEV void ring_or5(uint32_t *ring, uint32_t q, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4) {
-  if (q + 4u < G::kDw) {
+  if (q >= G::kMirror && q + 4u < G::kDw) {
     uint32_t *p = ring + q;
     atomicOr(p + 0, w0);
     atomicOr(p + 1, w1);
@@ -1425,11 +1433,11 @@ SB_DEV void ring_or5(uint32_t *ring, uint32_t q, uint32_t w0, uint32_t w1, uint3
     atomicOr(p + 3, w3);
     atomicOr(p + 4, w4);
   } else {
-    atomicOr(ring + (q & G::kDwMask), w0);
-    atomicOr(ring + ((q + 1u) & G::kDwMask), w1);
-    atomicOr(ring + ((q + 2u) & G::kDwMask), w2);
-    atomicOr(ring + ((q + 3u) & G::kDwMask), w3);
-    atomicOr(ring + ((q + 4u) & G::kDwMask), w4);
+    ring_or1<G>(ring, q & G::kDwMask, w0);
+    ring_or1<G>(ring, (q + 1u) & G::kDwMask, w1);
+    ring_or1<G>(ring, (q + 2u) & G::kDwMask, w2);
+    ring_or1<G>(ring, (q + 3u) & G::kDwMask, w3);
+    ring_or1<G>(ring, (q + 4u) & G::kDwMask, w4);
   }
 }
 
@@ -1438,7 +1446,7 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
                                                         const uint8_t *__restrict__ pool,
                                                         const int32_t *__restrict__ found) {
   using G = RingGeom<RB>;
-  __shared__ __attribute__((aligned(16))) uint32_t ring[G::kDw];
+  __shared__ __attribute__((aligned(16))) uint32_t ring[G::kDw + G::kMirror];
   __shared__ __attribute__((aligned(16))) uint32_t s_keep[17 * 4];  // s_keep[4n..4n+3]: mask of the low n bytes
   uint8_t *ring8 = reinterpret_cast<uint8_t *>(ring);
   const int lane = (int)threadIdx.x;
@@ -1482,7 +1490,14 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
     // ---- 2. zero the ring dwords of [Z, E)
     {
       const uint32_t z0 = (Gr + (uint32_t)Z) >> 2, z1 = (Gr + (uint32_t)E + 3u) >> 2;
-      for (uint32_t k = z0 + (uint32_t)lane; k < z1; k += 64u) ring[k & G::kDwMask] = 0u;
+#pragma unroll 1
+      for (uint32_t k0 = z0; k0 < z1; k0 += 64u) {  // (usually one or two rounds)
+        const uint32_t k = k0 + (uint32_t)lane, i = k & G::kDwMask;
+        if (k < z1) {
+          ring[i] = 0u;
+          if (i < G::kMirror) ring[G::kDw + i] = 0u;
+        }
+      }
       Z = (int)(z1 * 4u - Gr);
     }
     // ---- 3a. literals (before the match when a lane has both)
@@ -1492,8 +1507,8 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
       const uint32_t v = lv & (Ll >= 2 ? 0xffffu : 0xffu);
       const uint32_t x = (Gr + (uint32_t)O) & G::kMask, q = x >> 2, s8 = (x & 3u) * 8u;
       const uint64_t sv = (uint64_t)v << s8;
-      atomicOr(ring + q, (uint32_t)sv);
-      if ((uint32_t)(sv >> 32)) atomicOr(ring + ((q + 1u) & G::kDwMask), (uint32_t)(sv >> 32));
+      ring_or1<G>(ring, q, (uint32_t)sv);
+      if ((uint32_t)(sv >> 32)) ring_or1<G>(ring, (q + 1u) & G::kDwMask, (uint32_t)(sv >> 32));
     }
     // ---- 3b. matches, in rounds
     const int mO = O + (bLen ? nl : 0);
@@ -1527,17 +1542,8 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
             v0 = x.x; v1 = x.y; v2 = x.z; v3 = x.w;
           } else {
             const uint32_t xs = (Gr + (uint32_t)src) & G::kMask, qs = xs >> 2, ss = xs & 3u;
-            uint32_t s0, s1, s2, s3, s4;
-            if (qs + 4u < G::kDw) {
-              const uint32_t *p = ring + qs;
-              s0 = p[0]; s1 = p[1]; s2 = p[2]; s3 = p[3]; s4 = p[4];
-            } else {
-              s0 = ring[qs];
-              s1 = ring[(qs + 1u) & G::kDwMask];
-              s2 = ring[(qs + 2u) & G::kDwMask];
-              s3 = ring[(qs + 3u) & G::kDwMask];
-              s4 = ring[(qs + 4u) & G::kDwMask];
-            }
+            const uint32_t *p = ring + qs;  // (qs + 4 < kDw + kMirror: the mirror covers the wrap)
+            const uint32_t s0 = p[0], s1 = p[1], s2 = p[2], s3 = p[3], s4 = p[4];
             v0 = __builtin_amdgcn_alignbyte(s1, s0, ss);
             v1 = __builtin_amdgcn_alignbyte(s2, s1, ss);
             v2 = __builtin_amdgcn_alignbyte(s3, s2, ss);
