@@ -146,7 +146,7 @@ def main():
     ap.add_argument("--cpu-sample-mb", type=float, default=2000.0,
                     help="compressed MB of the same synthetic file timed on the CPU oracle (~10 s at 16 threads)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--e2e-windows", type=int, default=4,
+    ap.add_argument("--e2e-windows", type=int, default=6,
                     help="windows of the pinned-host → results measurement (0 = skip it)")
     ap.add_argument("--e2e-steps", type=int, default=2)
     ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EEDBA11)

@@ -300,7 +300,15 @@ int sbam_load(sbam_ctx *c, const uint8_t *data, int64_t len, int64_t base_offset
   HIPCHK(c, hipStreamSynchronize(c->stream));  // the previous window's work is done with d_comp
   HIPCHK(c, ensure(&c->d_comp, &c->comp_cap, (size_t)len + kCompPad));
   HIPCHK(c, hipMemsetAsync(c->d_comp + len, 0, kCompPad, c->stream));
-  if (len) HIPCHK(c, hipMemcpyAsync(c->d_comp, data, (size_t)len, hipMemcpyHostToDevice, c->stream));
+  // in 8 MiB pieces, each waited for: a multi-GB copy queued whole would hold the copy engine, and the small
+  // copies of another context's kernels running meanwhile (results, tables) would wait behind it
+  // (tools/e2e_probe.py: a window's compute 56 -> 98 ms while the next window's 2.5 GB copy ran)
+  constexpr int64_t kPiece = 8ll << 20;
+  for (int64_t o = 0; o < len; o += kPiece) {
+    const int64_t n = std::min(kPiece, len - o);
+    HIPCHK(c, hipMemcpyAsync(c->d_comp + o, data + o, (size_t)n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   // another file (or a range from its start): its contig lengths must come from sbam_header /
   // sbam_set_contig_lengths again; a later window of the same file keeps them
