@@ -235,7 +235,7 @@ def main():
     if W > 1:
         from concurrent.futures import ThreadPoolExecutor
         fill_pool = ThreadPoolExecutor(max_workers=threads)
-        pinned = [None, None]
+        pinned = [None] * sdist.WindowPipe.NBUF
 
         def stage_synth(lo, hi, j):
             if pinned[j] is None or pinned[j].numel() < hi - lo:

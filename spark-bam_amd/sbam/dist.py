@@ -362,45 +362,63 @@ def run_file(path, split_size: Optional[int] = None, world: Optional[int] = None
 
 class WindowPipe:
     """A rank's byte range streamed through two contexts in W windows (`wplans`: the windows' ShardPlans): while
-    window w computes on one context, a loader thread makes window w+1's bytes resident in the other (host
-    staging by `stage(lo, hi, j)` into context j's buffer, then sbam_load's host → device copy).  A step starts
-    with window 0 loaded in the foreground, so every step is a complete host → results pass.  `run_window(shard)`
-    is the per-window work (GpuShard.step / load_step / anything on shard.f)."""
+    window w computes on one context, a loader thread copies window w+1's bytes into the other (sbam_load's host →
+    device copy) and a stager thread stages window w+2 into host memory (`stage(lo, hi, k)` into staging buffer
+    k = w mod 3).  A step starts with window 0 loaded in the foreground, so every step is a complete host →
+    results pass.  `run_window(shard)` is the per-window work (GpuShard.step / load_step / anything on shard.f).
+    Buffer k is restaged only after the copy that read it has finished (window w+2 reuses window w-1's buffer,
+    whose copy ended before window w-1 computed)."""
+    NBUF = 3
 
     def __init__(self, wplans, stage, split_size, contig_lengths, device, run_window, halo: int = 2 << 20):
         from concurrent.futures import ThreadPoolExecutor
         self.wplans, self.stage, self.split_size = wplans, stage, split_size
         self.contig_lengths, self.device, self.run_window, self.halo = contig_lengths, device, run_window, halo
         self.loader = ThreadPoolExecutor(max_workers=1)
+        self.stager = ThreadPoolExecutor(max_workers=1)
         self.ctx = [None, None]
 
-    def _load(self, w, j):
+    def _range(self, w):
+        sh = self.ctx[w % 2]
+        return self.wplans[w].load_range(sh.halo if sh is not None else self.halo)
+
+    def _stage(self, w):
+        lo, hi = self._range(w)
+        return lo, hi, self.stage(lo, hi, w % self.NBUF)
+
+    def _load(self, w, staged):
         wp = self.wplans[w]
-        sh = self.ctx[j]
-        lo, hi = wp.load_range(sh.halo if sh is not None else self.halo)
-        buf = self.stage(lo, hi, j)
-        if sh is None:
-            self.ctx[j] = GpuShard(wp, lambda a, b: buf if (a, b) == (lo, hi) else self.stage(a, b, j),
+        j, k = w % 2, w % self.NBUF
+        lo, hi, buf = staged.result()
+        if (lo, hi) != self._range(w):  # the context's halo grew since staging: stage again
+            lo, hi = self._range(w)
+            buf = self.stage(lo, hi, k)
+        if self.ctx[j] is None:
+            self.ctx[j] = GpuShard(wp, lambda a, b: buf if (a, b) == (lo, hi) else self.stage(a, b, k),
                                    self.split_size, self.contig_lengths, device=self.device, halo=self.halo)
         else:
-            sh.reload(wp, buf)
+            self.ctx[j].reload(wp, buf)
         return self.ctx[j]
 
     def step(self) -> list:
         W = len(self.wplans)
         out = []
+        staged = {w: self.stager.submit(self._stage, w) for w in range(min(2, W))}
+        sh = self._load(0, staged[0])
         fut = None
-        sh = self._load(0, 0)
         for w in range(W):
             if w > 0:
                 sh = fut.result()
             if w + 1 < W:
-                fut = self.loader.submit(self._load, w + 1, (w + 1) % 2)
+                fut = self.loader.submit(self._load, w + 1, staged[w + 1])
+            if w + 2 < W:
+                staged[w + 2] = self.stager.submit(self._stage, w + 2)
             out.append(self.run_window(sh))
         return out
 
     def close(self):
         self.loader.shutdown()
+        self.stager.shutdown()
         for sh in self.ctx:
             if sh is not None:
                 sh.close()
