@@ -302,7 +302,7 @@ def main():
         log(f"[rank {rank}] PARITY PROPERTY FAILED: {parity}")
 
     # --- roofline of the dominant kernel (this rank's shard; per launch).  Candidates are single kernels:
-    # k_check<0, 1> (record-0 pass over the interior tiles: reads U, writes the U/8 PASS0 bitmap),
+    # k_check_bits (full-check record-0 pass over the interior tiles: reads U, writes the U/8 PASS0 bitmap),
     # k_inflate_decode (reads the C payload; its token stream is an internal intermediate) and
     # k_inflate_resolve (writes U; tokens internal).
     U, nblocks = last["U"], last["nblocks"]
@@ -312,7 +312,7 @@ def main():
         comp_payload = plan.owned_hi - plan.lo
     avg = {k: tot_ms[k] / args.steps for k in kernels}
     alg = {"check_pass0": U + U // 8, "inflate_decode": comp_payload, "inflate_resolve": U}
-    names = {"check_pass0": "k_check<0, 1>", "inflate_decode": "k_inflate_decode",
+    names = {"check_pass0": "k_check_bits", "inflate_decode": "k_inflate_decode",
              "inflate_resolve": "k_inflate_resolve"}
     if args.workload == "load-reads":
         del alg["check_pass0"]

@@ -13,8 +13,10 @@
 // position is checked against the window; a CIGAR scan is a masked ctz over the bitmap (16 ops per 64-bit
 // word) instead of a per-lane loop whose wave cost is the slowest lane; read names are checked 4 bytes at a
 // time (SWAR).  Positions whose first record passes (true starts and rare near-misses) continue the
-// 10-record chain from global memory.  Counts are accumulated per lane in carry-save bit planes (19 flags)
-// and packed 8-bit key counters, reduced with ballots once per 7 tiles.
+// 10-record chain from global memory.  The full check's Counts pass over interior tiles (k_check_bits) is
+// bit-sliced: each per-position predicate is a bit of a per-lane 32-position plane, the reference-index
+// predicates are evaluated once per byte offset and shared by the four positions that read that int32, and flags,
+// keys and PASS0 bits are counted / formed on whole planes.
 #include <algorithm>
 #include <atomic>
 #include <type_traits>
@@ -597,37 +599,6 @@ SB_DEV uint32_t check_first(const Tile &t, const StreamView &sv, const int32_t *
   return w;
 }
 
-// check_first<false, true> without its rare tails, branch-free: a name body or an op array longer than the 64
-// bytes / ops one bitmap read covers sets `rare` (the caller redoes that position with check_first).  Returns the
-// flag word F (0: record 0 passed).  With no branch inside, the four positions of a lane form one basic block
-// that the scheduler can interleave (a compare → select chain per position otherwise waits on its own VCC).
-SB_DEV uint32_t check_first_int(const Tile &t, const int32_t *lensL, int32_t nref, int rel, const int32_t f[8],
-                                const uint64_t *lomask, uint64_t nbm, bool &rare) {
-  const int32_t bs = f[0], ri = f[1], rp = f[2], bmn = f[3], fnc = f[4], ls = f[5], nri = f[6], nrp = f[7];
-  const int32_t lrn = bmn & 0xff;
-  const uint32_t flag = ((uint32_t)fnc) >> 16;
-  const int32_t nc = fnc & 0xffff;
-  const uint32_t rb0 = ref_bits_lds(ri, rp, lensL, nref), rb1 = ref_bits_lds(nri, nrp, lensL, nref);
-  const bool empty_mapped = (flag & 4u) == 0 && (ls == 0 || nc == 0);
-  const bool has_name = lrn >= 2;
-  const uint32_t last = t.win[rel + 35 + lrn];  // (read for lrn < 2 too, unused then)
-  const bool scan = has_name && last == 0;
-  const int32_t nbody = lrn - 1;
-  nbm &= lomask[nbody < 0 ? 0 : nbody > 64 ? 64 : nbody];  // lomask[n]: the low n bits
-  const int crel = rel + 36 + (has_name ? lrn : 0);
-  const uint64_t om = bits64(t.opc + (crel & 3) * kOpcWords, crel >> 2);
-  const bool inv_op = (om & lomask[nc > 64 ? 64 : nc]) != 0;  // an invalid op among the first min(nc, 64)
-  rare = (scan && nbm == 0 && nbody > 64) || (om == 0 && nc > 64);
-  uint32_t F = (rb0 << 1) | (rb1 << 5) | (too_few_remaining(bs, lrn, nc, ls) ? (1u << 18) : 0u);
-  F |= lrn == 0 ? (1u << 12) : 0u;
-  F |= lrn == 1 ? (1u << 13) : 0u;
-  F |= (has_name && last != 0) ? (1u << 10) : 0u;
-  F |= (scan && nbm != 0) ? (1u << 11) : 0u;
-  F |= inv_op ? (1u << 15) : 0u;
-  F |= (empty_mapped && !inv_op) ? (((ls == 0) ? (1u << 16) : 0u) | ((nc == 0) ? (1u << 17) : 0u)) : 0u;
-  return F;
-}
-
 // Stage the window of the tile at `base` (32 B per lane per step) and build the op-class and name-character
 // bitmaps (struct Tile).
 SB_DEV void stage_tile(const StreamView &sv, int64_t base, uint8_t *s_win, uint32_t *s_opc, uint32_t *s_nbad) {
@@ -901,51 +872,15 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
 #pragma unroll
       for (int q = 0; q < 10; q++) W[q] = w32[g + q];
       uint32_t wd[4];
-      if constexpr (INTERIOR && MODE == MODE_COUNTS) {
-        // branch-free record-0 checks of the 4 positions, then one wave-uniform fix-up for the rare long tails
-        bool rr[4];
-        // the name-character bitmap from bit 4g + 36 on, read once for the 4 positions (bits 4g + 36 + o ..)
-        const int nb0 = 4 * g + 36, nw = nb0 >> 5;
-        const uint32_t n0 = s_nbad[nw], n1 = s_nbad[nw + 1], n2 = s_nbad[nw + 2], n3 = s_nbad[nw + 3];
 #pragma unroll
-        for (int o = 0; o < 4; o++) {
-          int32_t f[8];
+      for (int o = 0; o < 4; o++) {
+        const int64_t x = xg + o;
+        int32_t f[8];
 #pragma unroll
-          for (int q = 0; q < 8; q++) f[q] = o == 0 ? (int32_t)W[q] : (int32_t)__builtin_amdgcn_alignbyte(W[q + 1], W[q], o);
-          const uint32_t sb = (uint32_t)(nb0 + o) & 31u;  // bit offset in n0.. (the +o may carry into n1)
-          const bool up = (nb0 & 31) + o >= 32;
-          const uint32_t a0 = up ? n1 : n0, a1 = up ? n2 : n1, a2 = up ? n3 : n2;
-          const uint64_t nbm = ((uint64_t)__builtin_amdgcn_alignbit(a2, a1, sb) << 32) | __builtin_amdgcn_alignbit(a1, a0, sb);
-          const uint32_t F = check_first_int(tl, lensL, sv.nref, 4 * g + o, f, s_lomask, nbm, rr[o]);
-          wd[o] = (F && R > 0) ? F : W_PASS0;
-        }
-        const uint32_t rm = (rr[0] ? 1u : 0u) | (rr[1] ? 2u : 0u) | (rr[2] ? 4u : 0u) | (rr[3] ? 8u : 0u);
-        if (__ballot(rm != 0u)) {  // (one copy of the exact path, looped: it must not cost registers)
-#pragma unroll 1
-          for (int o = 0; o < 4; o++) {
-            if ((rm >> o) & 1u) {
-              int32_t f[8];
-#pragma unroll
-              for (int q = 0; q < 8; q++) f[q] = (int32_t)__builtin_amdgcn_alignbyte(W[q + 1], W[q], (uint32_t)o);
-              const uint32_t w = check_first<false, true>(tl, sv, lensL, xg + o, 4 * g + o, R, f);
-              wd[0] = o == 0 ? w : wd[0];
-              wd[1] = o == 1 ? w : wd[1];
-              wd[2] = o == 2 ? w : wd[2];
-              wd[3] = o == 3 ? w : wd[3];
-            }
-          }
-        }
-      } else {
-#pragma unroll
-        for (int o = 0; o < 4; o++) {
-          const int64_t x = xg + o;
-          int32_t f[8];
-#pragma unroll
-          for (int q = 0; q < 8; q++) f[q] = o == 0 ? (int32_t)W[q] : (int32_t)__builtin_amdgcn_alignbyte(W[q + 1], W[q], o);
-          uint32_t w = check_first<EAGER, INTERIOR>(tl, sv, lensL, x, 4 * g + o, R, f);
-          if (!INTERIOR) w = (x >= x0 && x < x1) ? w : W_NONE;  // interior tiles lie inside [x0, x1)
-          wd[o] = w;
-        }
+        for (int q = 0; q < 8; q++) f[q] = o == 0 ? (int32_t)W[q] : (int32_t)__builtin_amdgcn_alignbyte(W[q + 1], W[q], o);
+        uint32_t w = check_first<EAGER, INTERIOR>(tl, sv, lensL, x, 4 * g + o, R, f);
+        if (!INTERIOR) w = (x >= x0 && x < x1) ? w : W_NONE;  // interior tiles lie inside [x0, x1)
+        wd[o] = w;
       }
       if (MODE == MODE_WORDS) {
 #pragma unroll
@@ -1036,6 +971,250 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
     for (int i = threadIdx.x; i < 19 * 19; i += kCheckThreads)
       if (s_pair[i]) atomicAdd(&cd.pair[i], (unsigned long long)s_pair[i]);
   }
+}
+
+// ---- full-check Counts over interior tiles, bit-sliced ------------------------------------------------------------
+// k_check<MODE_COUNTS, *> evaluates a position's 19 flags into one word and counts the words.  Here the positions
+// are the bits: lane t of the workgroup owns the 32 positions 1024 j + 4 t + o (j < 8, o < 4) of a tile, and every
+// per-position predicate becomes one bit of a per-lane "plane" (bit 31 - (4 j + o), appended by one v_addc:
+// plane + plane + the predicate's lane mask as carry-in).  Then
+//   * the reference-index predicates depend on one int32 each (PosChecker.scala:43-63): refIdx / refPos at x + 4 /
+//     x + 8, nextRefIdx / nextRefPos at x + 24 / x + 28.  A predicate pass evaluates "I(y) < -1", "I(y) >= n_ref"
+//     and "0 <= I(y) < n_ref && I(y + 4) > len[I(y)]" once per byte offset y into three LDS plane arrays; y = x + 4k
+//     is lane t + k's position, so flags 1-8 of lane t are those arrays at t + 1, t + 2, t + 6, t + 7 (3 predicate
+//     evaluations per position instead of 8);
+//   * the per-record predicates (read name, CIGAR, the implied length, the EmptyMapped fields) are evaluated per
+//     position (full/Checker.scala:22-184) and appended;
+//   * the 32 positions' flags combine as whole planes: per-flag totals are 16 v_bcnt; the key (number of flags) is a
+//     carry-save sum of 8 planes of mutually exclusive flag groups (at most one flag of each group holds at a
+//     position), decoded per key with one 3-input op and counted by v_bcnt; PASS0 is the NOR of the planes,
+//     transposed across 8 lanes (ds_swizzle) into bitmap dwords.
+// A position with a long name or op array (past the 64 bytes / ops one bitmap read covers) is redone by check_first
+// and patched into the planes.  Interior tiles only (no EOF in reach), R > 0, n_ref <= kLdsLens (lengths in LDS).
+SB_DEV uint32_t push_bit(uint32_t p, bool c) {
+  uint32_t r;
+  uint64_t co;
+  asm("v_addc_co_u32 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(p), "s"(__ballot(c)));
+  return r;
+}
+// One stage of an 8 x 8 transpose of nibbles across 8 lanes (nibble j of lane li -> nibble li of lane j): exchange
+// with lane li ^ S the nibbles j whose bit S differs from li's.
+template <int S>
+SB_DEV uint32_t nibble_xpose_stage(uint32_t P, int li) {
+  const uint32_t Q = (uint32_t)__builtin_amdgcn_ds_swizzle((int)P, 0x1f | (S << 10));
+  constexpr uint32_t Ms = S == 4 ? 0xffff0000u : S == 2 ? 0xff00ff00u : 0xf0f0f0f0u;  // nibbles j with j & S
+  const bool hi = (li & S) != 0;
+  const uint32_t r = __builtin_amdgcn_alignbit(Q, Q, hi ? 4 * S : 32 - 4 * S);
+  return hi ? ((P & Ms) | (r & ~Ms)) : ((P & ~Ms) | (r & Ms));
+}
+// plane i of X[] holds flag kBitFlag[i] (the flags an interior position can fail)
+constexpr int kBitFlag[16] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 13, 15, 16, 17, 18};
+
+__global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_INT) void k_check_bits(StreamView sv, int64_t x0, int R,
+                                                                                   CountsDev cd,
+                                                                                   unsigned long long *__restrict__ bitmap,
+                                                                                   int64_t tlo, int64_t thi) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_win[kWin + 64];
+  __shared__ uint32_t s_opc[4 * kOpcWords];
+  __shared__ uint32_t s_nbad[kNameWords];
+  __shared__ uint32_t s_pl[3][kCheckThreads + 8];  // per lane: I < -1, I >= n_ref, 0 <= I < n_ref && I(+4) > len[I]
+  __shared__ unsigned long long s_acc[19 + 21];     // totals, positions per key
+  __shared__ uint32_t s_k12[3 * 19];
+  __shared__ uint32_t s_pair[19 * 19];
+  __shared__ uint64_t s_lomask[65];
+  extern __shared__ int32_t s_lens[];  // the n_ref contig lengths (dynamic, >= 1 entry)
+  const int t = (int)threadIdx.x, lane = lane_id(), li = t & 7;
+  for (int i = t; i < 65; i += kCheckThreads) s_lomask[i] = i >= 64 ? ~0ull : (1ull << i) - 1ull;
+  for (int i = t; i < 3 * 19; i += kCheckThreads) s_k12[i] = 0;
+  for (int i = t; i < 19 * 19; i += kCheckThreads) s_pair[i] = 0;
+  for (int i = t; i < 19 + 21; i += kCheckThreads) s_acc[i] = 0;
+  const int32_t nref = sv.nref;
+  for (int i = t; i < nref; i += kCheckThreads) s_lens[i] = (int32_t)sv.lens[i];
+  const int64_t x0a = x0 & ~(int64_t)63;
+  const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
+  uint32_t ctot[16], ckey[8];
+#pragma unroll
+  for (int i = 0; i < 16; i++) ctot[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) ckey[i] = 0;
+
+  for (int64_t ti = blockIdx.x; ti < thi - tlo; ti += gridDim.x) {
+    const int64_t base = x0a + (tlo + ti) * kTile;
+    __syncthreads();
+    stage_tile(sv, base, s_win, s_opc, s_nbad);
+    __syncthreads();
+    // ---- predicate pass over the offsets 1024 j + 4 t + o; lanes t < 8 add row 8 (offsets 8192 + 4 t + o), which
+    // shifts row 0 out and leaves exactly the planes of lanes 256 + t
+    {
+      uint32_t pa = 0, pb = 0, pc = 0;
+      auto row = [&](int j) {
+        const int g = j * kCheckThreads + t;
+        const uint32_t W0 = w32[g], W1 = w32[g + 1], W2 = w32[g + 2];
+#pragma unroll
+        for (int o = 0; o < 4; o++) {
+          const int32_t I = (int32_t)(o == 0 ? W0 : __builtin_amdgcn_alignbyte(W1, W0, o));
+          const int32_t I4 = (int32_t)(o == 0 ? W1 : __builtin_amdgcn_alignbyte(W2, W1, o));
+          const bool in = (uint32_t)I < (uint32_t)nref;
+          const int32_t len = s_lens[in ? I : 0];
+          pa = push_bit(pa, I < -1);
+          pb = push_bit(pb, I >= nref);
+          pc = push_bit(pc, in && I4 > len);
+        }
+      };
+#pragma unroll 1
+      for (int j = 0; j < 8; j++) row(j);
+      s_pl[0][t] = pa;
+      s_pl[1][t] = pb;
+      s_pl[2][t] = pc;
+      if (t < 8) {
+        row(8);
+        s_pl[0][kCheckThreads + t] = pa;
+        s_pl[1][kCheckThreads + t] = pb;
+        s_pl[2][kCheckThreads + t] = pc;
+      }
+    }
+    __syncthreads();
+    // ---- per-record predicates
+    uint32_t pLZ = 0, pNB = 0, pIV = 0, pTF = 0, pRR = 0, pZ = 0, pO = 0, pFL = 0, pLS = 0, pNC = 0;
+#pragma unroll 1
+    for (int j = 0; j < 8; j++) {
+      const int g = j * kCheckThreads + t;
+      uint32_t W[7];
+#pragma unroll
+      for (int q = 0; q < 7; q++) W[q] = w32[g + q];
+      // the name-character bitmap from bit 4g + 36 on, read once for the 4 positions
+      const int nb0 = 4 * g + 36, nw = nb0 >> 5;
+      const uint32_t n0 = s_nbad[nw], n1 = s_nbad[nw + 1], n2 = s_nbad[nw + 2], n3 = s_nbad[nw + 3];
+#pragma unroll
+      for (int o = 0; o < 4; o++) {
+        const int rel = 4 * g + o;
+        auto fld = [&](int q) { return o == 0 ? W[q] : __builtin_amdgcn_alignbyte(W[q + 1], W[q], o); };
+        const int32_t bs = (int32_t)fld(0);
+        const int32_t lrn = (int32_t)((W[3] >> (8 * o)) & 0xffu);
+        const uint32_t fnc = fld(4);
+        const int32_t nc = (int32_t)(fnc & 0xffffu);
+        const int32_t ls = (int32_t)fld(5);
+        const uint32_t last = s_win[rel + 35 + lrn];  // the name's last byte (read for lrn < 2 too, unused then)
+        const uint32_t sb = (uint32_t)(nb0 + o) & 31u;
+        const bool up = (nb0 & 31) + o >= 32;
+        const uint32_t a0 = up ? n1 : n0, a1 = up ? n2 : n1, a2 = up ? n3 : n2;
+        uint64_t nbm = ((uint64_t)__builtin_amdgcn_alignbit(a2, a1, sb) << 32) | __builtin_amdgcn_alignbit(a1, a0, sb);
+        const int32_t nbody = lrn - 1;
+        nbm &= s_lomask[nbody < 0 ? 0 : nbody > 64 ? 64 : nbody];
+        const int crel = rel + 36 + (lrn >= 2 ? lrn : 0);
+        const uint64_t om = bits64(s_opc + (crel & 3) * kOpcWords, crel >> 2);
+        const bool inv = (om & s_lomask[nc > 64 ? 64 : nc]) != 0;  // an invalid op among the first min(nc, 64)
+        pLZ = push_bit(pLZ, last == 0);
+        pNB = push_bit(pNB, nbm != 0);
+        pIV = push_bit(pIV, inv);
+        pTF = push_bit(pTF, too_few_remaining(bs, lrn, nc, ls));
+        pRR = push_bit(pRR, (lrn > 65 && last == 0 && nbm == 0) || (om == 0 && nc > 64));
+        pZ = push_bit(pZ, lrn == 0);
+        pO = push_bit(pO, lrn == 1);
+        pFL = push_bit(pFL, ((fnc >> 18) & 1u) != 0);  // flag & 4 (segment unmapped)
+        pLS = push_bit(pLS, ls == 0);
+        pNC = push_bit(pNC, nc == 0);
+      }
+    }
+    // ---- flag planes
+    const uint32_t HN = ~(pZ | pO);  // l_read_name >= 2
+    uint32_t X[16];
+    X[0] = s_pl[0][t + 1];          // 1  refIdx < -1
+    X[1] = s_pl[1][t + 1];          // 2  refIdx >= n_ref
+    X[2] = s_pl[0][t + 2];          // 3  refPos < -1
+    X[3] = s_pl[2][t + 1];          // 4  refPos > len[refIdx]
+    X[4] = s_pl[0][t + 6];          // 5-8 the same for nextRefIdx / nextRefPos
+    X[5] = s_pl[1][t + 6];
+    X[6] = s_pl[0][t + 7];
+    X[7] = s_pl[2][t + 6];
+    X[8] = HN & ~pLZ;               // 10 name not NUL-terminated
+    X[9] = HN & pLZ & pNB;          // 11 non-ASCII name
+    X[10] = pZ;                     // 12 no read name
+    X[11] = pO;                     // 13 empty read name
+    X[12] = pIV;                    // 15 invalid CIGAR op
+    X[13] = ~pFL & pLS & ~pIV;      // 16 EmptyMapped: no sequence
+    X[14] = ~pFL & pNC & ~pIV;      // 17 EmptyMapped: no CIGAR ops
+    X[15] = pTF;                    // 18 too few remaining bytes for the implied length
+    if (__ballot(pRR != 0u)) {      // the long-name / long-CIGAR positions, exactly
+      const Tile tl{s_win, s_opc, s_nbad, base};
+      uint32_t m = pRR;
+      while (m) {
+        const int b = __builtin_ctz(m);
+        m &= m - 1u;
+        const int k = 31 - b, rel = 4 * ((k >> 2) * kCheckThreads + t) + (k & 3), d = rel >> 2;
+        int32_t f[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) f[q] = (int32_t)__builtin_amdgcn_alignbyte(w32[d + q + 1], w32[d + q], (uint32_t)(rel & 3));
+        const uint32_t w = check_first<false, true>(tl, sv, s_lens, base + rel, rel, R, f);
+        const uint32_t F = w == W_PASS0 ? 0u : w;
+#pragma unroll
+        for (int i = 0; i < 16; i++) X[i] = (X[i] & ~(1u << b)) | (((F >> kBitFlag[i]) & 1u) << b);
+      }
+    }
+    // ---- counting: per-flag totals, then the key from 8 planes of mutually exclusive flags
+#pragma unroll
+    for (int i = 0; i < 16; i++) ctot[i] += (uint32_t)__popc(X[i]);
+    const uint32_t Y0 = X[0] | X[1] | X[3], Y1 = X[2];      // {1, 2, 4}: refIdx < -1 / >= n_ref / in range
+    const uint32_t Y2 = X[4] | X[5] | X[7], Y3 = X[6];
+    const uint32_t Y4 = X[8] | X[9] | X[10] | X[11];         // {10, 11, 12, 13}: by l_read_name and the last byte
+    const uint32_t Y5 = X[12] | X[13], Y6 = X[14], Y7 = X[15];  // {15, 16}: by the invalid-op test
+    auto fa = [](uint32_t a, uint32_t b, uint32_t c, uint32_t &s) {
+      s = a ^ b ^ c;
+      return (a & b) | (c & (a ^ b));
+    };
+    uint32_t s1, s2, s3, s5;
+    const uint32_t c1 = fa(Y0, Y1, Y2, s1), c2 = fa(Y3, Y4, Y5, s2), c3 = fa(s1, s2, Y6, s3);
+    const uint32_t b0 = s3 ^ Y7, c4 = s3 & Y7;
+    const uint32_t c5 = fa(c1, c2, c3, s5);
+    const uint32_t b1 = s5 ^ c4, c6 = s5 & c4;
+    const uint32_t b2 = c5 ^ c6, b3 = c5 & c6;  // key = b0 + 2 b1 + 4 b2 + 8 b3 <= 8 (b3: key 8, the rest 0)
+    const uint32_t K1 = b0 & ~b1 & ~b2, K2 = ~b0 & b1 & ~b2;
+    ckey[0] += (uint32_t)__popc(K1);
+    ckey[1] += (uint32_t)__popc(K2);
+    ckey[2] += (uint32_t)__popc(b0 & b1 & ~b2);
+    ckey[3] += (uint32_t)__popc(~b0 & ~b1 & b2);
+    ckey[4] += (uint32_t)__popc(b0 & ~b1 & b2);
+    ckey[5] += (uint32_t)__popc(~b0 & b1 & b2);
+    ckey[6] += (uint32_t)__popc(b0 & b1 & b2);
+    ckey[7] += (uint32_t)__popc(b3);
+    if (__ballot((K1 | K2) != 0u)) {  // keys 1-2: per-flag counts and close-call pairs (rare)
+      uint32_t m = K1 | K2;
+      while (m) {
+        const int b = __builtin_ctz(m);
+        m &= m - 1u;
+        uint32_t F = 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++) F |= ((X[i] >> b) & 1u) << kBitFlag[i];
+        uint32_t oh;
+        classify_interior(F, s_k12, s_pair, oh);
+      }
+    }
+    // ---- PASS0 bits (no flag): bit 4 j + o after the reversal; an 8 x 8 nibble transpose across lanes t ^ 4, 2, 1
+    // leaves lane li of each 8-lane group with row j = li of the group's 32 positions
+    uint32_t P = __builtin_bitreverse32(~(Y0 | Y1 | Y2 | Y3 | Y4 | Y5 | Y6 | Y7));
+    P = nibble_xpose_stage<4>(P, li);
+    P = nibble_xpose_stage<2>(P, li);
+    P = nibble_xpose_stage<1>(P, li);
+    reinterpret_cast<uint32_t *>(bitmap)[((base - x0a) >> 5) + 32 * li + (t >> 3)] = P;
+  }
+  // per-lane counters -> workgroup -> device
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const uint32_t v = wave_sum(ctot[i]);
+    if (lane == 0 && v) atomicAdd(&s_acc[kBitFlag[i]], (unsigned long long)v);
+  }
+#pragma unroll
+  for (int k = 1; k <= 8; k++) {
+    const uint32_t v = wave_sum(ckey[k - 1]);
+    if (lane == 0 && v) atomicAdd(&s_acc[19 + k], (unsigned long long)v);
+  }
+  __syncthreads();
+  if (t < 19 && s_acc[t]) atomicAdd(&cd.totals[t], s_acc[t]);
+  if (t >= 32 && t < 53 && s_acc[19 + t - 32]) atomicAdd(&cd.positions[t - 32], s_acc[19 + t - 32]);
+  for (int i = t; i < 3 * 19; i += kCheckThreads)
+    if (s_k12[i]) atomicAdd(&cd.counts[i], (unsigned long long)s_k12[i]);
+  for (int i = t; i < 19 * 19; i += kCheckThreads)
+    if (s_pair[i]) atomicAdd(&cd.pair[i], (unsigned long long)s_pair[i]);
 }
 
 // ---- eager record-0 pass over interior tiles, with a prefilter -------------------------------------------------
@@ -1285,6 +1464,18 @@ static int resident_grid(int64_t ntiles) {
   return (int)(ntiles < 1 ? 1 : ntiles < want ? ntiles : want);
 }
 
+// Grid of k_check_bits over ntiles interior tiles (same policy as resident_grid; the occupancy depends on the
+// dynamic LDS of the contig lengths).
+static int bits_grid(int64_t ntiles, size_t shmem) {
+  int per_cu = 0, cus = 0, dev = 0;
+  (void)hipGetDevice(&dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_check_bits, kCheckThreads, shmem) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+  const int64_t want = std::max<int64_t>((int64_t)per_cu * cus, std::min<int64_t>(ntiles / 40, 131072));
+  return (int)(ntiles < 1 ? 1 : ntiles < want ? ntiles : want);
+}
 // Record-0 pass of mode MODE over [x0, x1): interior tiles by k_check<MODE, 1>, the rest by k_check<MODE, 2>.
 template <int MODE>
 static void launch_split_check(StreamView sv, int64_t x0, int64_t x1, int32_t R, CountsDev cd,
@@ -1308,11 +1499,26 @@ static int chain_grid(int64_t x0, int64_t x1) {
 hipError_t launch_check_full_counts(StreamView sv, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,
                                     unsigned long long *bitmap, hipStream_t s) {
   if (x1 <= x0) return hipSuccess;
-  if (by_key)
+  if (by_key) {
     hipLaunchKernelGGL((k_check<MODE_BYKEY, 0>), dim3(check_grid(ntiles_of(x0, x1))), dim3(kCheckThreads), 0, s, sv,
                        x0, x1, R, cd, bitmap, nullptr, (int64_t)0, (int64_t)0);
-  else
-    launch_split_check<MODE_COUNTS>(sv, x0, x1, R, cd, bitmap, s);
+  } else if (R > 0 && sv.nref <= kLdsLens) {
+    // interior tiles bit-sliced (k_check_bits), the boundary tiles by k_check<MODE_COUNTS, 2>
+    int64_t tlo, thi;
+    interior_tiles(sv, x0, x1, &tlo, &thi);
+    const int64_t nt = ntiles_of(x0, x1), ni = thi - tlo;
+    if (ni > 0) {
+      const size_t shmem = (size_t)std::max<int32_t>(sv.nref, 1) * sizeof(int32_t);
+      hipLaunchKernelGGL(k_check_bits, dim3(bits_grid(ni, shmem)), dim3(kCheckThreads), shmem, s, sv, x0, R, cd,
+                         bitmap, tlo, thi);
+    }
+    if (nt > ni)
+      hipLaunchKernelGGL((k_check<MODE_COUNTS, 2>), dim3(check_grid(nt - ni)), dim3(kCheckThreads), 0, s, sv, x0, x1,
+                         R, cd, bitmap, nullptr, tlo, thi);
+  } else {  // Success(0) everywhere, or contig lengths past the LDS table: the general pass
+    hipLaunchKernelGGL((k_check<MODE_COUNTS, 0>), dim3(check_grid(ntiles_of(x0, x1))), dim3(kCheckThreads), 0, s, sv,
+                       x0, x1, R, cd, bitmap, nullptr, (int64_t)0, (int64_t)0);
+  }
   return hipGetLastError();
 }
 hipError_t launch_check_full_chains(StreamView sv, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,

@@ -18,7 +18,7 @@ import os
 import statistics
 from collections import defaultdict
 
-KERNELS = {"k_check<0, 1>": "sbam::k_check<0, 1>", "k_check<0, 2>": "sbam::k_check<0, 2>",
+KERNELS = {"k_check_bits": "sbam::k_check_bits", "k_check<0, 0>": "sbam::k_check<0, 0>", "k_check<0, 2>": "sbam::k_check<0, 2>",
            "k_p0_links": "sbam::k_p0_links", "k_p0_list": "sbam::k_p0_list", "k_p0_count": "sbam::k_p0_count",
            "k_inflate_decode": "sbam::k_inflate_wave", "k_inflate_slow": "sbam::k_inflate_slow",
            "k_inflate_resolve": "sbam::k_inflate_resolve<12>", "k_check<1, 0>": "sbam::k_check<1, 0>",
