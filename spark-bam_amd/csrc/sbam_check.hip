@@ -472,13 +472,14 @@ typedef const __attribute__((address_space(1))) uint8_t *gbytes;
 SB_DEV gbytes gview(const uint8_t *p) { return (gbytes)p; }
 
 // The staged tile: bytes, plus two bitmaps built while staging —
-//   opc[r] (r = 0..3): bit k = "(win[4k + r] & 0xf) > 8", i.e. CIGAR op k of any op array starting at a byte
+//   opc, residue class r (r = 0..3), interleaved (class r's dword w at 4 w + r, so op_bits addresses it from the
+//     byte offset alone): bit k = "(win[4k + r] & 0xf) > 8", i.e. CIGAR op k of any op array starting at a byte
 //     offset ≡ r (mod 4) is invalid (Checker.MAX_CIGAR_OP; only an op's first byte matters): one 64-bit read
 //     covers 64 consecutive ops;
 //   nbad: bit r = "win[r] is not an allowed read-name character" (Checker.allowedReadNameChars).
 struct Tile {
   const uint8_t *win;     // staged bytes: win[r] = u[base + r], r < kWin
-  const uint32_t *opc;    // 4 × kOpcWords dwords
+  const uint32_t *opc;    // 4 × kOpcWords dwords (interleaved)
   const uint32_t *nbad;   // kNameWords dwords
   int64_t base;
 };
@@ -489,6 +490,15 @@ SB_DEV uint64_t bits64(const uint32_t *bm, int x) {
   const uint32_t s = (uint32_t)x & 31u;
   const uint32_t a = bm[w], b = bm[w + 1], c = bm[w + 2];
   return ((uint64_t)__builtin_amdgcn_alignbit(c, b, s) << 32) | __builtin_amdgcn_alignbit(b, a, s);
+}
+
+// Op-validity bits of the 64 ops at byte offsets c, c + 4, ... (bit i: op i invalid) from the interleaved class
+// bitmap: class c & 3, bit c >> 2 -> dword 4 (c >> 7) + (c & 3), shift (c >> 2) & 31.
+SB_DEV uint64_t op_bits(const uint32_t *opc, int c) {
+  const int w = ((c >> 5) & ~3) | (c & 3);
+  const uint32_t s = ((uint32_t)c >> 2) & 31u;
+  const uint32_t a = opc[w], b = opc[w + 4], d = opc[w + 8];
+  return ((uint64_t)__builtin_amdgcn_alignbit(d, b, s) << 32) | __builtin_amdgcn_alignbit(b, a, s);
 }
 
 // Any byte of the name body [rel, rel + n) outside allowedReadNameChars? (n <= 254, inside the window)
@@ -504,7 +514,7 @@ SB_DEV bool name_has_bad(const Tile &t, int rel, int32_t n) {
 // Index of the first op among the first `lim` ops at c, c+4, ... whose first byte has (b & 0xf) > 8, or lim.
 SB_DEV int32_t first_bad_op(const Tile &t, const StreamView &sv, int64_t c, int32_t lim) {
   const int rel = (int)(c - t.base);
-  const uint64_t m = bits64(t.opc + (rel & 3) * kOpcWords, rel >> 2);
+  const uint64_t m = op_bits(t.opc, rel);
   if (m) {
     const int32_t b = (int32_t)__builtin_ctzll(m);
     return b < lim ? b : lim;
@@ -565,7 +575,7 @@ SB_DEV uint32_t check_first(const Tile &t, const StreamView &sv, const int32_t *
     n_eof = n_eof64 < 0 ? 0 : n_eof64 > 0x7fffffff ? 0x7fffffff : (int32_t)n_eof64;
   }
   const int32_t lim = n_eof < nc ? n_eof : nc;
-  const uint64_t om = bits64(t.opc + (crel & 3) * kOpcWords, crel >> 2);
+  const uint64_t om = op_bits(t.opc, crel);
   int32_t bad = om ? (int32_t)__builtin_ctzll(om) : 64;
   if (om == 0 && lim > 64 && !name_eof) bad = first_bad_op(t, sv, c, lim);
   const bool inv_op = nc > 0 && bad < lim;
@@ -621,11 +631,11 @@ SB_DEV void stage_tile(const StreamView &sv, int64_t base, uint8_t *s_win, uint3
       nb |= (((m * 0x00204081u) >> 21) & 0xfu) << (4 * j);
     }
 #pragma unroll
-    for (int r = 0; r < 4; r++) opc8[r * 4 * kOpcWords + i] = (uint8_t)(T >> (8 * r));
+    for (int r = 0; r < 4; r++) opc8[16 * (i >> 2) + 4 * r + (i & 3)] = (uint8_t)(T >> (8 * r));
     s_nbad[i] = nb;
   }
   if (threadIdx.x < 4) s_nbad[kWin / 32 + threadIdx.x] = 0;
-  if (threadIdx.x < 16) s_opc[(threadIdx.x >> 2) * kOpcWords + kWin / 128 + (threadIdx.x & 3)] = 0;
+  if (threadIdx.x < 16) s_opc[kWin / 32 + threadIdx.x] = 0;  // the 4 pad words of every class
 }
 
 // ---- the tiled kernel -------------------------------------------------------------------------------------
@@ -831,9 +841,7 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
   __shared__ uint32_t s_cnt[BYKEY ? 21 * 19 : 1];
   __shared__ uint32_t s_k12[3 * 19];    // keys 0-2 × flag (non-BYKEY modes)
   __shared__ uint32_t s_pair[19 * 19];  // close-call pairs (key 2)
-  __shared__ uint64_t s_lomask[65];     // s_lomask[n] = the low n bits
   const int lane = lane_id();
-  for (int i = threadIdx.x; i < 65; i += kCheckThreads) s_lomask[i] = i >= 64 ? ~0ull : (1ull << i) - 1ull;
   for (int i = threadIdx.x; i < 3 * 19; i += kCheckThreads) s_k12[i] = 0;
   for (int i = threadIdx.x; i < 19 * 19; i += kCheckThreads) s_pair[i] = 0;
   const int32_t *lensL = nullptr;
@@ -1007,6 +1015,13 @@ SB_DEV uint32_t nibble_xpose_stage(uint32_t P, int li) {
   const uint32_t r = __builtin_amdgcn_alignbit(Q, Q, hi ? 4 * S : 32 - 4 * S);
   return hi ? ((P & Ms) | (r & ~Ms)) : ((P & ~Ms) | (r & Ms));
 }
+// Index of the lowest set bit of hi:lo, 0xffffffff if none (v_ffbl's value for 0: two ffbl, an or, a min).
+SB_DEV uint32_t ffbl(uint32_t x) {  // (a cttz with a defined zero would add a compare and a select)
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+SB_DEV uint32_t ctz64(uint32_t lo, uint32_t hi) { return min(ffbl(lo), ffbl(hi) | 32u); }
 // plane i of X[] holds flag kBitFlag[i] (the flags an interior position can fail)
 constexpr int kBitFlag[16] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 13, 15, 16, 17, 18};
 
@@ -1021,15 +1036,13 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_INT) void k_check_bit
   __shared__ unsigned long long s_acc[19 + 21];     // totals, positions per key
   __shared__ uint32_t s_k12[3 * 19];
   __shared__ uint32_t s_pair[19 * 19];
-  __shared__ uint64_t s_lomask[65];
-  extern __shared__ int32_t s_lens[];  // the n_ref contig lengths (dynamic, >= 1 entry)
+  extern __shared__ int32_t s_lens[];  // the n_ref contig lengths, then INT_MAX (dynamic, n_ref + 1 entries)
   const int t = (int)threadIdx.x, lane = lane_id(), li = t & 7;
-  for (int i = t; i < 65; i += kCheckThreads) s_lomask[i] = i >= 64 ? ~0ull : (1ull << i) - 1ull;
   for (int i = t; i < 3 * 19; i += kCheckThreads) s_k12[i] = 0;
   for (int i = t; i < 19 * 19; i += kCheckThreads) s_pair[i] = 0;
   for (int i = t; i < 19 + 21; i += kCheckThreads) s_acc[i] = 0;
   const int32_t nref = sv.nref;
-  for (int i = t; i < nref; i += kCheckThreads) s_lens[i] = (int32_t)sv.lens[i];
+  for (int i = t; i <= nref; i += kCheckThreads) s_lens[i] = i < nref ? (int32_t)sv.lens[i] : 0x7fffffff;
   const int64_t x0a = x0 & ~(int64_t)63;
   const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
   uint32_t ctot[16], ckey[8];
@@ -1054,11 +1067,10 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_INT) void k_check_bit
         for (int o = 0; o < 4; o++) {
           const int32_t I = (int32_t)(o == 0 ? W0 : __builtin_amdgcn_alignbyte(W1, W0, o));
           const int32_t I4 = (int32_t)(o == 0 ? W1 : __builtin_amdgcn_alignbyte(W2, W1, o));
-          const bool in = (uint32_t)I < (uint32_t)nref;
-          const int32_t len = s_lens[in ? I : 0];
+          const int32_t len = s_lens[min((uint32_t)I, (uint32_t)nref)];  // INT_MAX unless 0 <= I < n_ref
           pa = push_bit(pa, I < -1);
           pb = push_bit(pb, I >= nref);
-          pc = push_bit(pc, in && I4 > len);
+          pc = push_bit(pc, I4 > len);
         }
       };
 #pragma unroll 1
@@ -1075,49 +1087,51 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_INT) void k_check_bit
     }
     __syncthreads();
     // ---- per-record predicates
-    uint32_t pLZ = 0, pNB = 0, pIV = 0, pTF = 0, pRR = 0, pZ = 0, pO = 0, pFL = 0, pLS = 0, pNC = 0;
+    uint32_t pLZ = 0, pIV = 0, pTF = 0, pNG = 0, pZ = 0, pO = 0, pFL = 0, pLS = 0, pNC = 0;
 #pragma unroll 1
     for (int j = 0; j < 8; j++) {
       const int g = j * kCheckThreads + t;
       uint32_t W[7];
 #pragma unroll
       for (int q = 0; q < 7; q++) W[q] = w32[g + q];
-      // the name-character bitmap from bit 4g + 36 on, read once for the 4 positions
-      const int nb0 = 4 * g + 36, nw = nb0 >> 5;
-      const uint32_t n0 = s_nbad[nw], n1 = s_nbad[nw + 1], n2 = s_nbad[nw + 2], n3 = s_nbad[nw + 3];
+      // flag & 4 (segment unmapped) of the 4 positions: bit 2 of bytes 18-21 (position o at nibble bit 3 - o)
+      pFL = (pFL << 4) | ((W[4] >> 15) & 8u) | ((W[4] >> 24) & 4u) | ((W[5] >> 1) & 2u) | ((W[5] >> 10) & 1u);
 #pragma unroll
       for (int o = 0; o < 4; o++) {
         const int rel = 4 * g + o;
         auto fld = [&](int q) { return o == 0 ? W[q] : __builtin_amdgcn_alignbyte(W[q + 1], W[q], o); };
         const int32_t bs = (int32_t)fld(0);
         const int32_t lrn = (int32_t)((W[3] >> (8 * o)) & 0xffu);
-        const uint32_t fnc = fld(4);
-        const int32_t nc = (int32_t)(fnc & 0xffffu);
+        const int32_t nc = (int32_t)(fld(4) & 0xffffu);
         const int32_t ls = (int32_t)fld(5);
         const uint32_t last = s_win[rel + 35 + lrn];  // the name's last byte (read for lrn < 2 too, unused then)
-        const uint32_t sb = (uint32_t)(nb0 + o) & 31u;
-        const bool up = (nb0 & 31) + o >= 32;
-        const uint32_t a0 = up ? n1 : n0, a1 = up ? n2 : n1, a2 = up ? n3 : n2;
-        uint64_t nbm = ((uint64_t)__builtin_amdgcn_alignbit(a2, a1, sb) << 32) | __builtin_amdgcn_alignbit(a1, a0, sb);
-        const int32_t nbody = lrn - 1;
-        nbm &= s_lomask[nbody < 0 ? 0 : nbody > 64 ? 64 : nbody];
-        const int crel = rel + 36 + (lrn >= 2 ? lrn : 0);
-        const uint64_t om = bits64(s_opc + (crel & 3) * kOpcWords, crel >> 2);
-        const bool inv = (om & s_lomask[nc > 64 ? 64 : nc]) != 0;  // an invalid op among the first min(nc, 64)
+        // first invalid op (0xffffffff: none among the 64 one bitmap read covers)
+        const uint64_t om = op_bits(s_opc, rel + 36 + (lrn >= 2 ? lrn : 0));
+        const uint32_t obad = ctz64((uint32_t)om, (uint32_t)(om >> 32));
         pLZ = push_bit(pLZ, last == 0);
-        pNB = push_bit(pNB, nbm != 0);
-        pIV = push_bit(pIV, inv);
+        pIV = push_bit(pIV, obad < (uint32_t)nc);  // an invalid op among the first min(nc, 64)
         pTF = push_bit(pTF, too_few_remaining(bs, lrn, nc, ls));
-        pRR = push_bit(pRR, (lrn > 65 && last == 0 && nbm == 0) || (om == 0 && nc > 64));
+        pNG = push_bit(pNG, nc > 64);  // op array past the 64 checked ops
         pZ = push_bit(pZ, lrn == 0);
         pO = push_bit(pO, lrn == 1);
-        pFL = push_bit(pFL, ((fnc >> 18) & 1u) != 0);  // flag & 4 (segment unmapped)
         pLS = push_bit(pLS, ls == 0);
         pNC = push_bit(pNC, nc == 0);
       }
     }
-    // ---- flag planes
+    // the name characters matter only where the name ends in NUL (true records and ~1/256 of the rest): those
+    // positions are checked one by one; rare = such a name whose first 64 body bytes are clean but which is longer,
+    // or an op array whose first 64 ops are valid but which is longer — both redone exactly below
     const uint32_t HN = ~(pZ | pO);  // l_read_name >= 2
+    uint32_t pNB = 0, pRR = pNG & ~pIV;
+    for (uint32_t q = HN & pLZ; q; q &= q - 1u) {
+      const int b = __builtin_ctz(q), k = 31 - b, rel = 4 * ((k >> 2) * kCheckThreads + t) + (k & 3);
+      const int32_t nbody = (int32_t)s_win[rel + 12] - 1;
+      const uint64_t nbm = bits64(s_nbad, rel + 36);
+      const bool bad = ctz64((uint32_t)nbm, (uint32_t)(nbm >> 32)) < (uint32_t)nbody;
+      pNB |= bad ? (1u << b) : 0u;
+      pRR |= (!bad && nbody > 64) ? (1u << b) : 0u;
+    }
+    // ---- flag planes
     uint32_t X[16];
     X[0] = s_pl[0][t + 1];          // 1  refIdx < -1
     X[1] = s_pl[1][t + 1];          // 2  refIdx >= n_ref
@@ -1508,7 +1522,7 @@ hipError_t launch_check_full_counts(StreamView sv, int64_t x0, int64_t x1, int32
     interior_tiles(sv, x0, x1, &tlo, &thi);
     const int64_t nt = ntiles_of(x0, x1), ni = thi - tlo;
     if (ni > 0) {
-      const size_t shmem = (size_t)std::max<int32_t>(sv.nref, 1) * sizeof(int32_t);
+      const size_t shmem = ((size_t)sv.nref + 1) * sizeof(int32_t);
       hipLaunchKernelGGL(k_check_bits, dim3(bits_grid(ni, shmem)), dim3(kCheckThreads), shmem, s, sv, x0, R, cd,
                          bitmap, tlo, thi);
     }
