@@ -30,6 +30,9 @@
 #ifndef SBAM_CHECK_WGS_INT
 #define SBAM_CHECK_WGS_INT 5
 #endif
+#ifndef SBAM_CHECK_WGS_BITS
+#define SBAM_CHECK_WGS_BITS 6  // k_check_bits (a few kernel constants spill, reloaded once per tile)
+#endif
 #ifndef SBAM_LDS_LENS
 #define SBAM_LDS_LENS 4096
 #endif
@@ -1025,7 +1028,7 @@ SB_DEV uint32_t ctz64(uint32_t lo, uint32_t hi) { return min(ffbl(lo), ffbl(hi) 
 // plane i of X[] holds flag kBitFlag[i] (the flags an interior position can fail)
 constexpr int kBitFlag[16] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 13, 15, 16, 17, 18};
 
-__global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_INT) void k_check_bits(StreamView sv, int64_t x0, int R,
+__global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bits(StreamView sv, int64_t x0, int R,
                                                                                    CountsDev cd,
                                                                                    unsigned long long *__restrict__ bitmap,
                                                                                    int64_t tlo, int64_t thi) {
@@ -1045,11 +1048,23 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_INT) void k_check_bit
   for (int i = t; i <= nref; i += kCheckThreads) s_lens[i] = i < nref ? (int32_t)sv.lens[i] : 0x7fffffff;
   const int64_t x0a = x0 & ~(int64_t)63;
   const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
-  uint32_t ctot[16], ckey[8];
+  // per-lane counters, two 16-bit halves per register: c < 16 = plane c's flag total, 16 + k - 1 = key k
+  // (at most 32 per tile: flushed every kBitsFlush tiles)
+  constexpr int kBitsFlush = 2047;
+  uint32_t cnt[12];
 #pragma unroll
-  for (int i = 0; i < 16; i++) ctot[i] = 0;
+  for (int i = 0; i < 12; i++) cnt[i] = 0;
+  auto add_cnt = [&](int c, uint32_t v) { cnt[c >> 1] += (c & 1) ? v << 16 : v; };
+  auto flush_cnt = [&]() {
 #pragma unroll
-  for (int i = 0; i < 8; i++) ckey[i] = 0;
+    for (int c = 0; c < 24; c++) {
+      const uint32_t v = wave_sum((cnt[c >> 1] >> (16 * (c & 1))) & 0xffffu);
+      if (lane == 0 && v) atomicAdd(&s_acc[c < 16 ? kBitFlag[c] : 19 + c - 15], (unsigned long long)v);
+    }
+#pragma unroll
+    for (int i = 0; i < 12; i++) cnt[i] = 0;
+  };
+  int since_flush = 0;
 
   for (int64_t ti = blockIdx.x; ti < thi - tlo; ti += gridDim.x) {
     const int64_t base = x0a + (tlo + ti) * kTile;
@@ -1119,17 +1134,22 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_INT) void k_check_bit
       }
     }
     // the name characters matter only where the name ends in NUL (true records and ~1/256 of the rest): those
-    // positions are checked one by one; rare = such a name whose first 64 body bytes are clean but which is longer,
-    // or an op array whose first 64 ops are valid but which is longer — both redone exactly below
+    // positions are checked one by one, and so are the op arrays longer than 64 ops whose first 64 are valid
+    const Tile tl{s_win, s_opc, s_nbad, base};
     const uint32_t HN = ~(pZ | pO);  // l_read_name >= 2
-    uint32_t pNB = 0, pRR = pNG & ~pIV;
+    uint32_t pNB = 0;
     for (uint32_t q = HN & pLZ; q; q &= q - 1u) {
       const int b = __builtin_ctz(q), k = 31 - b, rel = 4 * ((k >> 2) * kCheckThreads + t) + (k & 3);
       const int32_t nbody = (int32_t)s_win[rel + 12] - 1;
       const uint64_t nbm = bits64(s_nbad, rel + 36);
-      const bool bad = ctz64((uint32_t)nbm, (uint32_t)(nbm >> 32)) < (uint32_t)nbody;
+      bool bad = ctz64((uint32_t)nbm, (uint32_t)(nbm >> 32)) < (uint32_t)nbody;
+      if (!bad && nbody > 64) bad = name_has_bad(tl, rel + 36 + 64, nbody - 64);
       pNB |= bad ? (1u << b) : 0u;
-      pRR |= (!bad && nbody > 64) ? (1u << b) : 0u;
+    }
+    for (uint32_t q = pNG & ~pIV; q; q &= q - 1u) {
+      const int b = __builtin_ctz(q), k = 31 - b, rel = 4 * ((k >> 2) * kCheckThreads + t) + (k & 3);
+      const int32_t lrn = s_win[rel + 12], nc = (int32_t)s_win[rel + 16] | ((int32_t)s_win[rel + 17] << 8);
+      if (first_bad_op(tl, sv, base + rel + 36 + (lrn >= 2 ? lrn : 0), nc) < nc) pIV |= 1u << b;
     }
     // ---- flag planes
     uint32_t X[16];
@@ -1149,25 +1169,9 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_INT) void k_check_bit
     X[13] = ~pFL & pLS & ~pIV;      // 16 EmptyMapped: no sequence
     X[14] = ~pFL & pNC & ~pIV;      // 17 EmptyMapped: no CIGAR ops
     X[15] = pTF;                    // 18 too few remaining bytes for the implied length
-    if (__ballot(pRR != 0u)) {      // the long-name / long-CIGAR positions, exactly
-      const Tile tl{s_win, s_opc, s_nbad, base};
-      uint32_t m = pRR;
-      while (m) {
-        const int b = __builtin_ctz(m);
-        m &= m - 1u;
-        const int k = 31 - b, rel = 4 * ((k >> 2) * kCheckThreads + t) + (k & 3), d = rel >> 2;
-        int32_t f[8];
-#pragma unroll
-        for (int q = 0; q < 8; q++) f[q] = (int32_t)__builtin_amdgcn_alignbyte(w32[d + q + 1], w32[d + q], (uint32_t)(rel & 3));
-        const uint32_t w = check_first<false, true>(tl, sv, s_lens, base + rel, rel, R, f);
-        const uint32_t F = w == W_PASS0 ? 0u : w;
-#pragma unroll
-        for (int i = 0; i < 16; i++) X[i] = (X[i] & ~(1u << b)) | (((F >> kBitFlag[i]) & 1u) << b);
-      }
-    }
     // ---- counting: per-flag totals, then the key from 8 planes of mutually exclusive flags
 #pragma unroll
-    for (int i = 0; i < 16; i++) ctot[i] += (uint32_t)__popc(X[i]);
+    for (int i = 0; i < 16; i++) add_cnt(i, (uint32_t)__popc(X[i]));
     const uint32_t Y0 = X[0] | X[1] | X[3], Y1 = X[2];      // {1, 2, 4}: refIdx < -1 / >= n_ref / in range
     const uint32_t Y2 = X[4] | X[5] | X[7], Y3 = X[6];
     const uint32_t Y4 = X[8] | X[9] | X[10] | X[11];         // {10, 11, 12, 13}: by l_read_name and the last byte
@@ -1183,14 +1187,18 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_INT) void k_check_bit
     const uint32_t b1 = s5 ^ c4, c6 = s5 & c4;
     const uint32_t b2 = c5 ^ c6, b3 = c5 & c6;  // key = b0 + 2 b1 + 4 b2 + 8 b3 <= 8 (b3: key 8, the rest 0)
     const uint32_t K1 = b0 & ~b1 & ~b2, K2 = ~b0 & b1 & ~b2;
-    ckey[0] += (uint32_t)__popc(K1);
-    ckey[1] += (uint32_t)__popc(K2);
-    ckey[2] += (uint32_t)__popc(b0 & b1 & ~b2);
-    ckey[3] += (uint32_t)__popc(~b0 & ~b1 & b2);
-    ckey[4] += (uint32_t)__popc(b0 & ~b1 & b2);
-    ckey[5] += (uint32_t)__popc(~b0 & b1 & b2);
-    ckey[6] += (uint32_t)__popc(b0 & b1 & b2);
-    ckey[7] += (uint32_t)__popc(b3);
+    add_cnt(16, (uint32_t)__popc(K1));
+    add_cnt(17, (uint32_t)__popc(K2));
+    add_cnt(18, (uint32_t)__popc(b0 & b1 & ~b2));
+    add_cnt(19, (uint32_t)__popc(~b0 & ~b1 & b2));
+    add_cnt(20, (uint32_t)__popc(b0 & ~b1 & b2));
+    add_cnt(21, (uint32_t)__popc(~b0 & b1 & b2));
+    add_cnt(22, (uint32_t)__popc(b0 & b1 & b2));
+    add_cnt(23, (uint32_t)__popc(b3));
+    if (++since_flush == kBitsFlush) {
+      flush_cnt();
+      since_flush = 0;
+    }
     if (__ballot((K1 | K2) != 0u)) {  // keys 1-2: per-flag counts and close-call pairs (rare)
       uint32_t m = K1 | K2;
       while (m) {
@@ -1212,16 +1220,7 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_INT) void k_check_bit
     reinterpret_cast<uint32_t *>(bitmap)[((base - x0a) >> 5) + 32 * li + (t >> 3)] = P;
   }
   // per-lane counters -> workgroup -> device
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    const uint32_t v = wave_sum(ctot[i]);
-    if (lane == 0 && v) atomicAdd(&s_acc[kBitFlag[i]], (unsigned long long)v);
-  }
-#pragma unroll
-  for (int k = 1; k <= 8; k++) {
-    const uint32_t v = wave_sum(ckey[k - 1]);
-    if (lane == 0 && v) atomicAdd(&s_acc[19 + k], (unsigned long long)v);
-  }
+  flush_cnt();
   __syncthreads();
   if (t < 19 && s_acc[t]) atomicAdd(&cd.totals[t], s_acc[t]);
   if (t >= 32 && t < 53 && s_acc[19 + t - 32]) atomicAdd(&cd.positions[t - 32], s_acc[19 + t - 32]);
