@@ -46,3 +46,36 @@ def test_synthetic_every_offset_and_counts(synth_file):
         assert np.array_equal(bits, (w & 0x80000000) != 0)
         assert np.array_equal(c.pair_hist, pair_hist(w))
         assert np.array_equal(g.check_eager(0, o.L), (w & 0x80000000) != 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["many_contigs", "reads_to_check_0"])
+def test_counts_general_paths(synth_file, case):
+    """The bit-sliced interior pass (k_check_bits) needs R > 0 and the contig lengths in LDS (n_ref <= 4096); the
+    other cases run the general k_check<MODE_COUNTS, 0> over every tile.  Both against the oracle: 5000 contigs
+    (the 84 real ones, then 4916 more, so refIdx values up to 4999 become in-range) and reads_to_check = 0."""
+    import sbam
+    s, data, o = synth_file
+    R = 0 if case == "reads_to_check_0" else 10
+    lens, nref = o.lens, o.nref
+    try:
+        if case == "many_contigs":
+            rng = np.random.default_rng(7)
+            extra = rng.integers(1, 1 << 31, 5000 - o.nref).astype(np.int64)
+            o.lens = np.zeros(1 << 16, np.int64)
+            o.lens[:nref] = lens[:nref]
+            o.lens[nref:5000] = extra
+            o.nref = 5000
+        x1 = min(o.L, 6_000_000)
+        counts, npos, rbe, nsucc = o.counts_range(0, x1, R)
+        w = o.check_full_range(0, x1, R)
+        with sbam.BamFile(data, path="synth.bam", contig_lengths=o.lens[:o.nref]) as g:
+            c, bits = g.check_full_counts(0, x1, reads_to_check=R, want_bitmap=True)
+            assert np.array_equal(c.totals, counts.sum(0))
+            assert np.array_equal(c.by_key[:3], counts[:3])
+            assert np.array_equal(c.positions, npos)
+            assert np.array_equal(c.reads_before_error, rbe)
+            assert c.n_success == nsucc
+            assert np.array_equal(bits, (w & 0x80000000) != 0)
+    finally:
+        o.lens, o.nref = lens, nref
