@@ -31,7 +31,7 @@
 #define SBAM_CHECK_WGS_INT 5
 #endif
 #ifndef SBAM_CHECK_WGS_BITS
-#define SBAM_CHECK_WGS_BITS 6  // k_check_bits (a few kernel constants spill, reloaded once per tile)
+#define SBAM_CHECK_WGS_BITS 5  // k_check_bits (6 spills a few constants: +7 GB scratch traffic, same time)
 #endif
 #ifndef SBAM_LDS_LENS
 #define SBAM_LDS_LENS 4096
