@@ -33,6 +33,13 @@ SB_DEV int32_t rd_i32(const uint8_t *u, int64_t x) {
                    ((uint32_t)u[x + 3] << 24));
 }
 
+// the little-endian int32 at x from the two aligned dwords around it (the stream buffer is 4-byte aligned and
+// padded past L)
+SB_DEV int32_t rd_i32_aligned(const uint8_t *u, int64_t x) {
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(u + (x & ~(int64_t)3));
+  return (int32_t)__builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(x & 3));
+}
+
 // bit at stream offset x of a bitmap whose bit 0 is offset xa (xa 64-aligned)
 SB_DEV bool bm_test(const unsigned long long *bm, int64_t xa, int64_t x) {
   const int64_t r = x - xa;
@@ -53,6 +60,29 @@ SB_DEV bool bm_any(const unsigned long long *bm, int64_t xa, int64_t a, int64_t 
   return (bm[wb] & hi) != 0;
 }
 
+// The hop p -> q holds: no set bit in [p + 1, min(q, X1)) and, for q < X1, bit q set.  A record's span usually
+// covers a few bitmap words: those (up to 8) are loaded at once rather than one dependent load per word.
+SB_DEV bool hop_ok(const unsigned long long *bm, int64_t xa, int64_t p, int64_t q, int64_t X1) {
+  const int64_t e = q < X1 ? q : X1;
+  const int64_t ra = p + 1 - xa, re = e - xa, rq = q - xa;  // bits [ra, re) must be clear
+  const int64_t wa = ra >> 6, wl = (q < X1 ? rq : re - 1) >> 6;
+  if (re <= ra || wl - wa >= 8) return !bm_any(bm, xa, p + 1, e) && (q >= X1 || bm_test(bm, xa, q));
+  unsigned long long wv[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) wv[k] = wa + k <= wl ? bm[wa + k] : 0ull;
+  bool any = false, qset = q >= X1;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const int64_t b0 = (wa + k) << 6;  // first bit of the word
+    unsigned long long m = wv[k];
+    m &= ra > b0 ? ~0ull << (ra - b0) : ~0ull;
+    m &= re >= b0 + 64 ? ~0ull : re <= b0 ? 0ull : (1ull << (re - b0)) - 1ull;
+    any |= m != 0;
+    if (q < X1 && (rq >> 6) == wa + k) qset = (wv[k] >> (rq & 63)) & 1ull;
+  }
+  return !any && qset;
+}
+
 }  // namespace
 
 // One thread per bitmap word of [X0, X1): every set bit p in it must hop to the next set bit (or past X1).
@@ -70,12 +100,10 @@ __global__ void k_chain_proof(const uint8_t *__restrict__ u, int64_t L, const un
       const int64_t p = base + __builtin_ctzll(m);
       m &= m - 1;
       if (p + 4 > L) { bad = true; break; }
-      const int32_t bs = rd_i32(u, p);
+      const int32_t bs = rd_i32_aligned(u, p);
       const int64_t q = p + 4 + (int64_t)bs;
       if (bs < 0 || q > L) { bad = true; break; }
-      const int64_t e = q < X1 ? q : X1;
-      if (bm_any(bm, xa, p + 1, e)) bad = true;
-      else if (q < X1 && !bm_test(bm, xa, q)) bad = true;
+      if (!hop_ok(bm, xa, p, q, X1)) bad = true;
     }
     if (bad) atomicOr(fail, 1);
   }
