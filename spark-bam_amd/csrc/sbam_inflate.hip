@@ -1199,29 +1199,35 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
           }
         }
         entry = ((uint32_t)rp << 10) | ((uint32_t)stt << 9) | pl;
+        // one symbol, predicated: a lane that is done (stopped out of the data, or past its segment) decodes the
+        // same symbol again and commits nothing, so the steps need no exec-mask branches
         auto step = [&]() {
+          const bool live = go && rp < seg_end;
           const uint32_t p0 = (uint32_t)rp;
+          int rq = rp;
           uint32_t v;
-          const uint32_t kind = (wsym(L, wq, rp, stt, v) >> 8) & 3u;
-          const bool outp = rp > pend;
-          const bool stp = kind == K_SPEC || outp;
-          if (stp) {  // rare: record the stop (exit in the literal state | kind) and decode on
-            const uint32_t ek = ((uint32_t)rp << 10) | (uint32_t)(outp ? ST_OUT : v == 0 ? ST_EOB : ST_ERR);
+          const uint32_t kind = (wsym(L, wq, rq, stt, v) >> 8) & 3u;
+          const bool outp = rq > pend;
+          const bool stp = live && (kind == K_SPEC || outp);
+          if (__ballot(stp) != 0) {  // rare: record the stop (exit in the literal state | kind) and decode on
+            const uint32_t ek = ((uint32_t)rq << 10) | (uint32_t)(outp ? ST_OUT : v == 0 ? ST_EOB : ST_ERR);
             const uint32_t cn = tokA | (bytA << 12);
-            const bool w1 = nst == 0, w2 = nst == 1;
+            const bool w1 = stp && nst == 0, w2 = stp && nst == 1;
             s1p = w1 ? p0 : s1p;
             s1e = w1 ? ek : s1e;
             s1c = w1 ? cn : s1c;
             s2p = w2 ? p0 : s2p;
             s2e = w2 ? ek : s2e;
             s2c = w2 ? cn : s2c;
-            nst++;
-            go = !outp;
+            nst += stp ? 1 : 0;
+            go = (stp && outp) ? false : go;
           }
-          tokA += stp ? 0u : 1u;
-          bytA += stp ? 0u : kind == K_LIT ? 1u : kind == K_LEN ? v : 0u;
-          pl = (!stp && kind == K_LEN) ? v : pl;
-          stt = (!stp && kind == K_LEN) ? 1 : 0;
+          rp = live ? rq : rp;
+          const bool cnt = live && !stp;
+          tokA += cnt ? 1u : 0u;
+          bytA += cnt ? (kind == K_LIT ? 1u : kind == K_LEN ? v : 0u) : 0u;
+          pl = (cnt && kind == K_LEN) ? v : pl;
+          stt = live ? ((cnt && kind == K_LEN) ? 1 : 0) : stt;
         };
         // checkpoints every kCpSteps steps (wave-uniform, so a record costs no divergent branch): the lane's
         // position if it is at a literal/length boundary
@@ -1230,11 +1236,12 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
           const bool live = go && rp < seg_end;
           cp[jj] = (live && stt == 0) ? (uint32_t)rp : ~0u;
           cc[jj] = tokA | (bytA << 12);
+          if (__ballot(live) != 0) {
 #pragma unroll 1
-          for (int k = 0; k < kCpSteps; k++)
-            if (go && rp < seg_end) step();
+            for (int k = 0; k < kCpSteps; k++) step();
+          }
         });
-        while (go && rp < seg_end) step();
+        while (__ballot(go && rp < seg_end) != 0) step();
         exitEnd = ((uint32_t)rp << 10) | ((uint32_t)stt << 9) | pl;
       }
       WMARK(3);
