@@ -1237,7 +1237,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
           cp[jj] = (live && stt == 0) ? (uint32_t)rp : ~0u;
           cc[jj] = tokA | (bytA << 12);
           if (__ballot(live) != 0) {
-#pragma unroll 1
+#pragma unroll 2  // (4 and 8: the same; 1: +0.5 ms)
             for (int k = 0; k < kCpSteps; k++) step();
           }
         });
