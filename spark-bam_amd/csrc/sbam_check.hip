@@ -1322,7 +1322,7 @@ __global__ __launch_bounds__(kCheckThreads) void k_eager(StreamView sv, int64_t 
         if (eager_pass_direct(s_win, sv, lensL, base + rel, rel, f)) atomicOr(&s_bits[rel >> 6], 1ull << (rel & 63));
       }
     };
-    // prefilter: bit 4j + o of sm = position 4 (j·kCheckThreads + thread) + o survives
+    // prefilter: bit 31 - (4j + o) of sm = position 4 (j·kCheckThreads + thread) + o survives
     uint32_t sm = 0;
 #pragma unroll
     for (int j = 0; j < kTile / (4 * kCheckThreads); j++) {
@@ -1331,7 +1331,7 @@ __global__ __launch_bounds__(kCheckThreads) void k_eager(StreamView sv, int64_t 
 #pragma unroll
       for (int o = 0; o < 4; o++) {
         const uint32_t ri = __builtin_amdgcn_alignbyte(a2, a1, o), nri = __builtin_amdgcn_alignbyte(a7, a6, o);
-        sm |= (ri + 1u <= nref1 && nri + 1u <= nref1) ? (1u << (4 * j + o)) : 0u;
+        sm = push_bit(sm, ri + 1u <= nref1 && nri + 1u <= nref1);  // position (j, o) at bit 31 - (4 j + o)
       }
     }
     // queue the wave's survivors (kEagerQ at a time) and check them 64 at a time
@@ -1342,7 +1342,7 @@ __global__ __launch_bounds__(kCheckThreads) void k_eager(StreamView sv, int64_t 
       uint32_t at = incl - n;
       for (uint32_t m = sm; m && at < r0 + kEagerQ; m &= m - 1, at++) {
         if (at >= r0) {
-          const int bit = __builtin_ctz(m);
+          const int bit = 31 - __builtin_ctz(m);
           q[at - r0] = (uint16_t)(4 * ((bit >> 2) * kCheckThreads + (int)threadIdx.x) + (bit & 3));
         }
       }
