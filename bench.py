@@ -238,6 +238,8 @@ def main():
         pinned = [None] * sdist.WindowPipe.NBUF
 
         def stage_synth(lo, hi, j):
+            if j is None:  # a halo retry's private bytes (WindowPipe: never a shared staging slot)
+                return s.slice(lo, hi)
             if pinned[j] is None or pinned[j].numel() < hi - lo:
                 pinned[j] = torch.empty(int((hi - lo) * 1.05), dtype=torch.uint8, pin_memory=True)
             buf = pinned[j].numpy()[:hi - lo]

@@ -324,6 +324,7 @@ int sbam_reset(sbam_ctx *c) {
   c->ncand = -1;
   c->nblocks = -1;
   c->L = -1;
+  c->inflate_slow = -1;
   c->bm_valid = false;
   c->n_loaded = -1;
   c->err = sbam_error{};
@@ -553,7 +554,7 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
 
 int sbam_inflate_fallbacks(sbam_ctx *c, int64_t *n) {
   if (!c || !n) return SBAM_ERR_ARG;
-  if (c->L < 0 && c->inflate_slow < 0) return set_err(c, SBAM_ERR_STATE, "sbam_inflate has not run");
+  if (c->L < 0 || c->inflate_slow < 0) return set_err(c, SBAM_ERR_STATE, "sbam_inflate has not run");
   *n = c->inflate_slow;
   return SBAM_OK;
 }

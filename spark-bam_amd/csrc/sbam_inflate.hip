@@ -716,7 +716,14 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
 // ends before ISIZE or runs past it, a distance too far back — sends the block to k_inflate_slow (the exact
 // per-lane decoder), so zlib's semantics are unchanged.
 namespace wd {
-constexpr int kK = 512;                    // bits per lane segment
+// 544 bits = 17 dwords: lane k's window reads start at dword 17 k + drift, so the 32 lanes of a ds_read group land
+// in distinct banks (at 512 = 16 dwords, lanes k and k + 2 shared a bank: 20.9 G conflict cycles per launch at
+// 10 GB, 7.0 G at 544; decode 67.0 → 63.8 ms).  An XOR-swizzled root-table index changed nothing (62.3 vs 62.6 G
+// over three launches): the conflicts were the window reads'.
+#ifndef SBAM_KK
+#define SBAM_KK 544
+#endif
+constexpr int kK = SBAM_KK;                // bits per lane segment
 constexpr int kWinDw = 64 * kK / 32 + 16;  // staged input dwords per round (start alignment + lookahead)
 // A 9-bit literal/length root (zlib's choice: ENOUGH_LENS = 852 entries with sub-tables) keeps the wave's LDS at
 // 9.4 KiB, so 16 decoder waves fit a CU (a 10-bit root: 11.4 KiB, 14 waves, decode 86 → 79 ms at 10 GB).
@@ -750,6 +757,17 @@ struct WaveLds {
   SB_DEV uint8_t *lens() { return reinterpret_cast<uint8_t *>(win + wd::kWinDw - wd::kScratchDw); }  // [320]
   SB_DEV uint16_t *sorted() { return reinterpret_cast<uint16_t *>(win + wd::kWinDw - wd::kScratchDw + 80); }  // [320]
 };
+
+// Root-table slot of root index i (R root bits).  SBAM_TSWZ: XOR bits 5.. into bits 0..4, so that the 2^(R-l)
+// replicated entries of a short code no longer all share one LDS bank (bank = slot mod 32).
+template <int R>
+SB_DEV uint32_t root_slot(uint32_t i) {
+#ifdef SBAM_TSWZ
+  return i ^ ((i >> 5) & ((1u << (R - 5)) - 1u));
+#else
+  return i;
+#endif
+}
 
 SB_DEV uint32_t sym_entry(uint32_t s, uint32_t l, bool dist) {
   using namespace wd;
@@ -863,7 +881,7 @@ SB_DEV bool wave_build(WaveLds &L, int off, int nsym, int toff, int subcap) {
     const uint32_t v = (__builtin_bitreverse32((uint32_t)e) >> (32 - R)) << (15 - R);
     if (v < c.lim[R]) {
       const uint32_t l = canon_len(c, v);
-      tab[e] = sym_entry(sorted[off + (int)(v >> (15 - l)) + canon_base(c, l)], l, DIST);
+      tab[root_slot<R>((uint32_t)e)] = sym_entry(sorted[off + (int)(v >> (15 - l)) + canon_base(c, l)], l, DIST);
     }
   }
   // sub-tables: one per root prefix of the codes longer than R, sized by the longest code under that prefix
@@ -881,7 +899,7 @@ SB_DEV bool wave_build(WaveLds &L, int off, int nsym, int toff, int subcap) {
     const uint32_t incl = wave_incl_scan(sz);
     const int my = next + (int)(incl - sz);
     if (j < npre && my + (int)sz <= subcap) {
-      tab[__builtin_bitreverse32(P) >> (32 - R)] = wd::kSub | (sb << 11) | ((uint32_t)((1 << R) + my) << 16);
+      tab[root_slot<R>(__builtin_bitreverse32(P) >> (32 - R))] = wd::kSub | (sb << 11) | ((uint32_t)((1 << R) + my) << 16);
       for (uint32_t k = 0; k < sz; k++) {
         const uint32_t v = (P << (15 - R)) | ((__builtin_bitreverse32(k) >> (32 - sb)) << (15 - R - sb));
         const uint32_t l = canon_len(c, v);
@@ -904,7 +922,12 @@ SB_DEV uint32_t wsym(const WaveLds &L, int wq, int &pos, int st, uint32_t &v) {
   const uint32_t lo = __builtin_amdgcn_alignbit(L.win[w + 1], L.win[w], q & 31u);
   const uint32_t tb = st ? (uint32_t)kDistOff : (uint32_t)kLitOff;
   const uint32_t R = st ? (uint32_t)kDistRoot : (uint32_t)kLitRoot;
+#ifdef SBAM_TSWZ
+  const uint32_t ri = lo & ((1u << R) - 1u);
+  uint32_t e = L.tab[tb + (ri ^ ((ri >> 5) & (st ? 7u : 15u)))];
+#else
   uint32_t e = L.tab[tb + (lo & ((1u << R) - 1u))];
+#endif
   if (e & kSub) e = L.tab[tb + (e >> 16) + ((lo >> R) & ((1u << ((e >> 11) & 31u)) - 1u))];
   const uint32_t n = e & 15u, x = (e >> 4) & 15u;
   v = (e >> 16) + __builtin_amdgcn_ubfe(lo, n, x);
@@ -1198,6 +1221,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
             stt = kind == K_LEN ? 1 : 0;
           }
         }
+        WMARK(13);
         entry = ((uint32_t)rp << 10) | ((uint32_t)stt << 9) | pl;
         // one symbol, predicated: a lane that is done (stopped out of the data, or past its segment) decodes the
         // same symbol again and commits nothing, so the steps need no exec-mask branches
@@ -1616,9 +1640,9 @@ hipError_t launch_first_error(const int32_t *status, int64_t n, unsigned long lo
 
 hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *tok, int32_t *status,
                                  int32_t *found, int32_t *slow, unsigned int *counters, hipStream_t s) {
-  if (bt.n == 0) return hipSuccess;
-  // counters: [0] slow-path blocks, [1] slow-path work
+  // counters: [0] slow-path blocks, [1] slow-path work (zeroed first: the host reads [0] back even for 0 blocks)
   (void)hipMemsetAsync(counters, 0, 3 * sizeof(unsigned int), s);
+  if (bt.n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_inflate_wave, dim3((unsigned)bt.n), dim3(64), 0, s, d, D, bt, tok, status, found, slow,
                      counters + 0);
   hipLaunchKernelGGL(k_inflate_slow, dim3(256), dim3(kDecThreads), 0, s, d, D, bt, tok, slow, counters + 0, status,

@@ -324,11 +324,21 @@ class BamFile:
         `data` (numpy uint8, possibly a view of pinned host memory) must stay alive while loading."""
         buf = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
         self._buf = np.ascontiguousarray(buf)
+        file_size = int(file_size if file_size is not None else base_offset + self._buf.size)
+        # the context drops its contig lengths when the range may hold a different header (sbam_load)
+        drop = base_offset == 0 or file_size != self.file_size
         self.base_offset = base_offset
-        self.file_size = int(file_size if file_size is not None else base_offset + self._buf.size)
+        self.file_size = file_size
         self._check(self.L.sbam_load(self.ctx, _ptr(self._buf), self._buf.size, base_offset, self.file_size))
+        if drop:
+            self.n_ref = self.contig_lengths = self.header_end = None
         self.n_blocks = None
         self.uncompressed_size = None
+
+    @property
+    def loads_to_eof(self) -> bool:
+        """Whether the resident bytes reach the end of the file (else a scan past them is a halo miss)."""
+        return self.base_offset + self._buf.size >= self.file_size
 
     def reset(self):
         """Drop derived stages (keeps the resident compressed bytes and allocations)."""

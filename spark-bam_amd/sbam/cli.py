@@ -1,7 +1,7 @@
 """spark-bam CLI drop-ins over the GPU path: `full-check`, `check-bam -s`, `check-blocks -s`, `compute-splits -s`,
 `count-reads`, `index-blocks`, `index-records`.
 
-    python -m sbam.cli full-check [-l LIMIT] [-m SPLIT] [-i RANGES] [-r READS] BAM [OUT]
+    python -m sbam.cli full-check [-l LIMIT] [-m SPLIT] [-i RANGES] [-r READS] [--gpus N | --windows W] BAM [OUT]
     python -m sbam.cli check-bam -s [-l LIMIT] [-m SPLIT] [-i RANGES] BAM [OUT]
     python -m sbam.cli check-blocks -s [-l LIMIT] BAM [OUT]
     python -m sbam.cli index-blocks BAM [OUT]
@@ -28,6 +28,7 @@ import math
 import os
 import sys
 import time
+from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -133,19 +134,135 @@ def show_record(rec: bytes, contig_names: Sequence[str]) -> str:
 
 
 # ---- full-check ----------------------------------------------------------------------------------------------
-class FullCheckReport:
-    """full-check over the blocks selected by `ranges` (None = whole file)."""
+@dataclass
+class FullCheckParts:
+    """One byte range's share of a full-check report (the whole file, or one shard of `full-check --gpus N`):
+    Counts, the first `limit` close calls of keys 1 and 2 as PosMetadata lines, and the comparison with the
+    `.records` truth.  Parts of consecutive ranges merge in file order (merge_parts) — Spark's reduceByKey of Counts
+    and the driver's take(limit) of the sampled positions (FullCheck.scala:141-191, CheckerApp.scala:140-222)."""
+    totals: np.ndarray      # (19,)
+    by_key: np.ndarray      # (21, 19): keys 1-2 exact (the report prints only those)
+    positions: np.ndarray   # (21,)
+    rbe: np.ndarray         # (21, 128) readsBeforeError by key
+    pair: np.ndarray        # (19, 19) close-call flag pairs
+    n_positions: int
+    compressed: int
+    close: dict             # key -> PosMetadata lines of the first `limit` positions with that key
+    truth: Optional[dict]   # {"tp", "fp": [(F, PosMetadata line or None)], "fn": [Pos text]} with a .records file
 
-    def __init__(self, f: sbam.BamFile, data: bytes, records_path: Optional[str], limit: int = 10,
-                 ranges: Optional[List[Tuple[int, int]]] = None, reads_to_check: int = 10):
+
+def merge_parts(parts: Sequence[FullCheckParts], limit: int) -> FullCheckParts:
+    """Shards in file order → one report's parts (counts summed, sampled lines concatenated and cut to `limit`)."""
+    def add(name):
+        return sum(getattr(q, name) for q in parts)
+    close = {k: [ln for q in parts for ln in q.close.get(k, [])][:limit] for k in (1, 2)}
+    truth = None
+    if parts and all(q.truth is not None for q in parts):
+        fp = [x for q in parts for x in q.truth["fp"]]
+        truth = {"tp": sum(q.truth["tp"] for q in parts), "fp": fp,
+                 "fn": [x for q in parts for x in q.truth["fn"]]}
+    return FullCheckParts(add("totals"), add("by_key"), add("positions"), add("rbe"), add("pair"),
+                          add("n_positions"), add("compressed"), close, truth)
+
+
+def truth_lines(n_positions: int, compressed: int, tp: int, fps: Sequence[Tuple[int, Optional[str]]],
+                fns: Sequence[str], limit: int) -> List[str]:
+    """CheckerApp.scala:140-222: positions, compressed size, ratio, reads, then the comparison of the calls with the
+    `.records` truth (lines, false-positive flags histogram and sites, false-negative positions)."""
+    ratio = n_positions / compressed if compressed else float("nan")
+    out = [f"{n_positions} uncompressed positions", f"{format_bytes(compressed)} compressed",
+           "Compression ratio: %.2f" % ratio, f"{tp + len(fns)} reads"]
+    if not fps and not fns:
+        out.append("All calls matched!")
+        return out
+    out += [f"{len(fps)} false positives, {len(fns)} false negatives", ""]
+    if fps:
+        hist = {}
+        for F, _ in fps:
+            hist[F] = hist.get(F, 0) + 1
+        rows = sorted(hist.items(), key=lambda kv: -kv[1])
+        print_limited(out, [f"{n}:\t{show_flags(F)}" for F, n in rows], None,
+                      "False-positive-site flags histogram:", lambda _: "False-positive-site flags histogram:", limit)
+        out.append("")
+        items = [ln for _, ln in fps[:limit]]
+        print_limited(out, items, len(fps), "False positives with succeeding read info:",
+                      lambda n: f"{n} of {len(fps)} false positives with succeeding read info::", limit)
+    if fns:
+        print_limited(out, list(fns[:limit]), len(fns), f"{len(fns)} false negatives:",
+                      lambda n: f"{n} of {len(fns)} false negatives:", limit)
+    return out
+
+
+def full_check_lines(p: FullCheckParts, limit: int) -> List[str]:
+    """FullCheck.scala:141-322 report text from (merged) parts."""
+    out = []
+    if p.truth is not None:
+        fp, fn = p.truth["fp"], p.truth["fn"]
+        if fp or fn:  # FullCheck.scala:108-114: a full-check call disagreeing with the records is an error
+            raise RuntimeError(f"{len(fp)} false positives, {len(fn)} false negatives against the .records truth")
+        out += truth_lines(p.n_positions, p.compressed, p.truth["tp"], fp, fn, limit) + [""]
+    field_names = FLAG_NAMES[:19]
+
+    def pairs(vec):
+        return [(field_names[i], int(vec[i])) for i in range(19)]
+
+    npos = p.positions
+    if npos[1] > 0:  # critical (key-1) section, FullCheck.scala:230-258
+        out.append("Critical error counts (true negatives where only one check failed):")
+        out += ["\t" + l for l in count_lines(pairs(p.by_key[1]), False, False)]
+        out.append("")
+        n1 = int(npos[1])
+        print_limited(out, p.close[1], n1, f"{n1} critical positions:",
+                      lambda n: f"{n} of {n1} critical positions:", limit)
+    else:
+        out.append("No positions where only one check failed")
+    out.append("")
+    if npos[2] > 0:  # close calls (key 2), FullCheck.scala:262-306
+        n2 = int(npos[2])
+        print_limited(out, p.close[2], n2, f"{n2} positions where exactly two checks failed:",
+                      lambda n: f"{n} of {n2} positions where exactly two checks failed:", limit)
+        out.append("")
+        hist = []
+        for i in range(19):
+            for j in range(19):
+                if p.pair[i, j]:
+                    hist.append((int(p.pair[i, j]), (1 << i) | (1 << j)))
+        hist.sort(key=lambda t: -t[0])  # stable: reduceByKey output order is not pinned beyond the counts
+        if hist and hist[0][0] > 1:
+            print_limited(out, [f"{n}:\t{show_flags(F)}" for n, F in hist], None, "Histogram:",
+                          lambda _: "Histogram:", limit, indent="\t")
+            out.append("")
+        out.append("\tPer-flag totals:")
+        out += ["\t\t" + l for l in count_lines(pairs(p.by_key[2]), False, False)]
+        out.append("")
+    else:
+        out += ["No positions where exactly two checks failed", ""]
+    rb = [(k, int(p.rbe[:, k].sum())) for k in range(1, 128) if p.rbe[:, k].sum()]
+    out.append("Total error counts:")
+    out += ["\t" + l for l in count_lines(pairs(p.totals), True, True, rb)]
+    out.append("")
+    return out
+
+
+class FullCheckReport:
+    """full-check over the blocks selected by `ranges` (None = whole file) of one context.  `blocks` (a block-index
+    mask) restricts it further to the blocks a shard owns; `names` = the header's contig names (a shard's stream
+    does not start at the header)."""
+
+    def __init__(self, f: sbam.BamFile, data: Optional[bytes], records_path: Optional[str], limit: int = 10,
+                 ranges: Optional[List[Tuple[int, int]]] = None, reads_to_check: int = 10,
+                 blocks: Optional[np.ndarray] = None, names: Optional[List[str]] = None):
         self.f, self.data, self.limit, self.R = f, data, limit, reads_to_check
         st, cs, us, uo = f.blocks()
         sel = np.ones(st.size, bool) if ranges is None else \
             np.any([(st >= lo) & (st < hi) for lo, hi in ranges], axis=0)
+        if blocks is not None:
+            sel &= blocks
+        self.block_starts = set(st[sel].tolist())
         self.runs = self._runs(np.nonzero(sel)[0], uo, us)
         self.compressed = int(cs[sel].astype(np.int64).sum())
         self.records_path = records_path
-        self.names = header_names(f)
+        self.names = header_names(f) if names is None else names
 
     @staticmethod
     def _runs(idx, uo, us):
@@ -162,6 +279,8 @@ class FullCheckReport:
     def close_calls(self, key: int, want: int) -> List[Tuple[int, int]]:
         """First `want` positions (file order) whose result has exactly `key` non-zero fields."""
         got = []
+        if want <= 0:
+            return got
         chunk = 1 << 24
         for x0, x1 in self.runs:
             for a in range(x0, x1, chunk):
@@ -192,7 +311,8 @@ class FullCheckReport:
         return f"{p}:\t{desc}. Failing checks: {show_flags(w & 0x7ffff)}"
 
     def next_record(self, x: int, max_read_size: int = 10_000_000):
-        """FindRecordStart.withDelta(pos) (FindRecordStart.scala:30-63): first eager-true offset >= x."""
+        """FindRecordStart.withDelta(pos) (FindRecordStart.scala:30-63): first eager-true offset >= x.  A search that
+        runs past a shard's loaded bytes raises HaloException (the shard grows its halo and re-runs)."""
         L = self.f.uncompressed_size
         lim = min(L, x + max_read_size)
         a, step = x, 1 << 20
@@ -203,19 +323,22 @@ class FullCheckReport:
             if hit.size:
                 return a + int(hit[0]), a + int(hit[0]) - x
             a = b
+        if lim < x + max_read_size and not getattr(self.f, "loads_to_eof", True):
+            raise sbam.HaloException(f"next record after {x} lies past the loaded bytes")
         return None
 
     def truth(self) -> set:
+        """The `.records` positions (IndexRecords.scala) inside this report's blocks, as stream offsets."""
         out = set()
         for line in open(self.records_path):
             if line.strip():
                 b, o = (int(v) for v in line.split(","))
-                out.add(self.f.offset_of(Pos(b, o)))
+                if b in self.block_starts:
+                    out.add(self.f.offset_of(Pos(b, o)))
         return out
 
-    def summary(self, calls_bits, n_positions):
-        """CheckerApp.scala:140-222: positions, compressed size, ratio, reads, then the comparison of the calls
-        with the `.records` truth (lines, false-positive offsets, false-negative offsets)."""
+    def compare(self, calls_bits):
+        """(tp, false-positive offsets, false-negative offsets) of the calls against the `.records` truth."""
         truth = self.truth()
         tp, fps, fns = 0, [], []
         for x0, bits in calls_bits:
@@ -224,107 +347,50 @@ class FullCheckReport:
             tp += len(called & expected)
             fps += sorted(called - expected)
             fns += sorted(expected - called)
-        ratio = n_positions / self.compressed if self.compressed else float("nan")
-        out = [f"{n_positions} uncompressed positions", f"{format_bytes(self.compressed)} compressed",
-               "Compression ratio: %.2f" % ratio, f"{tp + len(fns)} reads"]
-        if not fps and not fns:
-            out.append("All calls matched!")
-            return out, fps, fns
-        out += [f"{len(fps)} false positives, {len(fns)} false negatives", ""]
-        if fps:
-            words = {x: int(self.f.check_full_words(x, x + 1, self.R)[0]) for x in fps}
-            hist = {}
-            for x in fps:
-                F = words[x] & 0x7ffff
-                hist[F] = hist.get(F, 0) + 1
-            rows = sorted(hist.items(), key=lambda kv: -kv[1])
-            print_limited(out, [f"{n}:\t{show_flags(F)}" for F, n in rows], None,
-                          "False-positive-site flags histogram:", lambda _: "False-positive-site flags histogram:",
-                          self.limit)
-            out.append("")
-            items = [self.pos_metadata(x, words[x]) for x in fps[:self.limit]]
-            print_limited(out, items, len(fps), "False positives with succeeding read info:",
-                          lambda n: f"{n} of {len(fps)} false positives with succeeding read info::", self.limit)
-        if fns:
-            print_limited(out, [str(self.f.pos_of(x)) for x in fns[:self.limit]], len(fns),
-                          f"{len(fns)} false negatives:", lambda n: f"{n} of {len(fns)} false negatives:", self.limit)
-        return out, fps, fns
+        return tp, fps, fns
+
+    def truth_part(self, calls_bits) -> dict:
+        tp, fps, fns = self.compare(calls_bits)
+        words = {x: int(self.f.check_full_words(x, x + 1, self.R)[0]) for x in fps}
+        fp = [(words[x] & 0x7ffff, self.pos_metadata(x, words[x]) if i < self.limit else None)
+              for i, x in enumerate(fps)]
+        return {"tp": tp, "fp": fp, "fn": [str(self.f.pos_of(x)) for x in fns]}
 
     def check_bam_lines(self) -> List[str]:
         """check-bam -s (eager/CheckBam.scala, vsIndexed): the eager checker at every position of the selected
         blocks against the `.records` truth."""
         calls_bits = [(x0, self.f.check_eager(x0, x1, self.R)) for x0, x1 in self.runs]
         n_positions = sum(x1 - x0 for x0, x1 in self.runs)
-        return self.summary(calls_bits, n_positions)[0]
+        t = self.truth_part(calls_bits)
+        return truth_lines(n_positions, self.compressed, t["tp"], t["fp"], t["fn"], self.limit)
 
-    def lines(self) -> List[str]:
-        f, out = self.f, []
-        counts = None
-        c_by_key = np.zeros((21, 19), np.int64)
+    def parts(self) -> FullCheckParts:
+        """The full checker over every position of the selected blocks (Counts by the bit-sliced counts path: keys
+        1-2 per flag, positions per key, pairs, readsBeforeError, totals) plus the sampled close calls."""
+        by_key = np.zeros((21, 19), np.int64)
         npos = np.zeros(21, np.int64)
         totals = np.zeros(19, np.int64)
         rbe = np.zeros((21, 128), np.int64)
         pair = np.zeros((19, 19), np.int64)
-        n_positions = n_success = 0
+        n_positions = 0
         calls_bits = []
+        has_truth = bool(self.records_path) and os.path.exists(self.records_path)
         for x0, x1 in self.runs:
-            c, bits = f.check_full_counts(x0, x1, self.R, want_bitmap=True, by_key=True)
-            c_by_key += c.by_key
+            c, bits = self.f.check_full_counts(x0, x1, self.R, want_bitmap=True)
+            by_key += c.by_key
             npos += c.positions
             totals += c.totals
             rbe += c.reads_before_error
             pair += c.pair_hist
             n_positions += x1 - x0
-            n_success += c.n_success
             calls_bits.append((x0, bits))
-        if self.records_path and os.path.exists(self.records_path):
-            head, fp, fn = self.summary(calls_bits, n_positions)
-            if fp or fn:  # FullCheck.scala:108-114: a full-check call disagreeing with the records is an error
-                raise RuntimeError(f"{len(fp)} false positives, {len(fn)} false negatives against {self.records_path}")
-            out += head + [""]
-        field_names = FLAG_NAMES[:19]
+        close = {k: [self.pos_metadata(x, w) for x, w in self.close_calls(k, min(self.limit, int(npos[k])))]
+                 for k in (1, 2)}
+        truth = self.truth_part(calls_bits) if has_truth else None
+        return FullCheckParts(totals, by_key, npos, rbe, pair, n_positions, self.compressed, close, truth)
 
-        def pairs(vec):
-            return [(field_names[i], int(vec[i])) for i in range(19)]
-
-        if npos[1] > 0:  # critical (key-1) section, FullCheck.scala:230-258
-            out.append("Critical error counts (true negatives where only one check failed):")
-            out += ["\t" + l for l in count_lines(pairs(c_by_key[1]), False, False)]
-            out.append("")
-            n1 = int(npos[1])
-            items = [self.pos_metadata(x, w) for x, w in self.close_calls(1, self.limit)]
-            print_limited(out, items, n1, f"{n1} critical positions:",
-                          lambda n: f"{n} of {n1} critical positions:", self.limit)
-        else:
-            out.append("No positions where only one check failed")
-        out.append("")
-        if npos[2] > 0:  # close calls (key 2), FullCheck.scala:262-306
-            n2 = int(npos[2])
-            items = [self.pos_metadata(x, w) for x, w in self.close_calls(2, self.limit)]
-            print_limited(out, items, n2, f"{n2} positions where exactly two checks failed:",
-                          lambda n: f"{n} of {n2} positions where exactly two checks failed:", self.limit)
-            out.append("")
-            hist = []
-            for i in range(19):
-                for j in range(19):
-                    if pair[i, j]:
-                        F = (1 << i) | (1 << j)
-                        hist.append((int(pair[i, j]), F))
-            hist.sort(key=lambda t: -t[0])  # stable: reduceByKey output order is not pinned beyond the counts
-            if hist and hist[0][0] > 1:
-                print_limited(out, [f"{n}:\t{show_flags(F)}" for n, F in hist], None, "Histogram:",
-                              lambda _: "Histogram:", self.limit, indent="\t")
-                out.append("")
-            out.append("\tPer-flag totals:")
-            out += ["\t\t" + l for l in count_lines(pairs(c_by_key[2]), False, False)]
-            out.append("")
-        else:
-            out += ["No positions where exactly two checks failed", ""]
-        rb = [(k, int(rbe[:, k].sum())) for k in range(1, 128) if rbe[:, k].sum()]
-        out.append("Total error counts:")
-        out += ["\t" + l for l in count_lines(pairs(totals), True, True, rb)]
-        out.append("")
-        return out
+    def lines(self) -> List[str]:
+        return full_check_lines(self.parts(), self.limit)
 
 
 def header_names(f: sbam.BamFile) -> List[str]:
@@ -417,8 +483,9 @@ def spawn_ranks(n: int, argv: Sequence[str]) -> int:
 
 
 def sharded_lines(a) -> Optional[List[str]]:
-    """compute-splits / count-reads over byte-range shards, one rank per GPU (sbam.dist.run_file: rank 0 reads the
-    header, each rank preads its shard, one all_gather + all_reduce).  Returns the report on rank 0, None elsewhere."""
+    """compute-splits / count-reads / full-check over byte-range shards, one rank per GPU (sbam.dist.run_file /
+    full_check_file: rank 0 reads the header, each rank preads its shard, the results meet in tiny collectives).
+    Returns the report on rank 0, None elsewhere."""
     import torch
     import torch.distributed as dist
     from sbam import dist as sdist
@@ -431,6 +498,10 @@ def sharded_lines(a) -> Optional[List[str]]:
         dist.init_process_group(a.dist_backend)
         coll = None
     try:
+        if a.cmd == "full-check":
+            parts = sdist.full_check_file(a.bam, a.print_limit, a.intervals, a.reads_to_check, device=local,
+                                          coll_device=coll, records_path=a.bam + ".records")
+            return full_check_lines(parts, a.print_limit) if dist.get_rank() == 0 else None
         t = time.perf_counter()
         r = sdist.run_file(a.bam, sbam.effective_split_size(a.max_split_size), device=local, coll_device=coll)
         ms = int((time.perf_counter() - t) * 1e3)
@@ -577,7 +648,10 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
             p.add_argument("-r", "--reads-to-check", type=int, default=10)
         if name in ("compute-splits", "check-bam", "check-blocks"):
             p.add_argument("-s", "--spark-bam", action="store_true")
-        if name in ("compute-splits", "count-reads"):
+        if name == "full-check":
+            p.add_argument("--windows", type=int, default=1,
+                           help="byte-range shards run one after another on one GPU (files larger than HBM)")
+        if name in ("compute-splits", "count-reads", "full-check"):
             p.add_argument("--gpus", type=int, default=1, help="byte-range shards, one rank per GPU")
             p.add_argument("--dist-backend", default="nccl", help="nccl (RCCL); gloo to rehearse ranks on one GPU")
             p.add_argument("--device", type=int, default=None, help="GPU of every rank (default LOCAL_RANK)")
@@ -592,6 +666,16 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
                 open(a.out, "w").write(text)
             else:
                 sys.stdout.write(text)
+        return 0
+    if a.cmd == "full-check" and a.windows > 1:
+        from sbam import dist as sdist
+        parts = sdist.full_check_file(a.bam, a.print_limit, a.intervals, a.reads_to_check, world=a.windows,
+                                      device=0, records_path=a.bam + ".records")
+        text = "\n".join(full_check_lines(parts, a.print_limit)) + "\n"
+        if a.out:
+            open(a.out, "w").write(text)
+        else:
+            sys.stdout.write(text)
         return 0
     data = open(a.bam, "rb").read()
     with sbam.BamFile(data, path=a.bam) as f:

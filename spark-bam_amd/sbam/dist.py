@@ -145,10 +145,13 @@ class GpuShard:
         self.f = self.sbam.BamFile(self.source(lo, hi), device=self.device, base_offset=lo,
                                    file_size=self.plan.file_size, inflate=False)
 
-    def reload(self, plan: ShardPlan, data: np.ndarray):
+    def reload(self, plan: ShardPlan, data: np.ndarray, source: Optional[Callable[[int, int], np.ndarray]] = None):
         """Stream the next byte-range window through this shard's context (sbam_load: device allocations are
-        kept): `data` = the bytes of plan.load_range(self.halo)."""
+        kept): `data` = the bytes of plan.load_range(self.halo).  `source` replaces the byte source a halo retry
+        reads from (it must not hand back a buffer another window is being staged into)."""
         self.plan = plan
+        if source is not None:
+            self.source = source
         lo, _ = plan.load_range(self.halo)
         self.f.load(data, base_offset=lo, file_size=plan.file_size)
 
@@ -156,6 +159,14 @@ class GpuShard:
         self.f.reset()
         self.f.run(contig_lengths=self.contig_lengths)
         return shard_pass(self.f, self.plan, self.split_size, self.R)
+
+    def run_with(self, fn):
+        """Any per-shard work fn(f, plan) on the shard's inflated stream, with the halo retry of step()."""
+        def once():
+            self.f.reset()
+            self.f.run(contig_lengths=self.contig_lengths)
+            return fn(self.f, self.plan)
+        return self._retry(once)
 
     def _retry(self, fn):
         while True:
@@ -329,7 +340,8 @@ def run_file(path, split_size: Optional[int] = None, world: Optional[int] = None
     import sbam
     split_size = sbam.effective_split_size(split_size)
     source, size = file_source(path) if isinstance(path, (str, os.PathLike)) else path
-    if _dist_ready():
+    grouped = _dist_ready()  # in a process group the collectives run even at world size 1 (RCCL exercised)
+    if grouped:
         import torch.distributed as dist
         world, rank = dist.get_world_size(), dist.get_rank()
         ranks = [rank]
@@ -341,7 +353,7 @@ def run_file(path, split_size: Optional[int] = None, world: Optional[int] = None
         device = 0 if device is None else device
     read_header = read_header or read_contig_lengths
     lens = read_header(source, size, device) if rank == 0 else None
-    if len(ranks) == 1 and world > 1:
+    if grouped:
         lens = broadcast_lengths(lens, coll_device)
     if open_shard is None:
         def open_shard(plan, src, ss, cl):
@@ -354,10 +366,107 @@ def run_file(path, split_size: Optional[int] = None, world: Optional[int] = None
             results.append(sh.step())
         finally:
             sh.close()
-    if len(ranks) == 1 and world > 1:
+    if grouped:
         results = gather_results(results[0], plans, device=coll_device)
     splits, sizes, counts = combine(results, size)
     return RunResult(splits, sizes, unpack_counts(counts), np.asarray(lens, np.int64))
+
+
+def owned_blocks(f, p: ShardPlan) -> np.ndarray:
+    """Block mask of the blocks shard `p` owns in its context `f`: from its first block up to the block where the next
+    shard's stream starts (FindBlockStart of that shard's first split), as shard_pass does."""
+    st = f.blocks()[0]
+    if p.owned_hi >= p.file_size:
+        return np.ones(st.size, bool)
+    b = int(np.searchsorted(st, f.find_block_start(p.owned_hi)))
+    m = np.zeros(st.size, bool)
+    m[:b] = True
+    return m
+
+
+def read_header_names(source, file_size: int, device: int = 0, probe: int = 1 << 20):
+    """(ContigLengths, contig names) from the header at the start of the file (bam/header/Header.scala:26-60)."""
+    import sbam
+    from sbam.cli import header_names
+    hi = min(file_size, probe)
+    while True:
+        try:
+            with sbam.BamFile(source(0, hi), device=device, file_size=file_size, inflate=False) as f:
+                f.inflate()
+                return f.header()[1], header_names(f)
+        except sbam.SbamError as e:
+            if "truncated header" not in str(e) or hi >= file_size:
+                raise
+            hi = min(file_size, 2 * hi)
+
+
+def _pack_parts_counts(q) -> np.ndarray:
+    return np.concatenate([q.totals, q.by_key.ravel(), q.positions, q.rbe.ravel(), q.pair.ravel(),
+                           np.array([q.n_positions, q.compressed], np.int64)]).astype(np.int64)
+
+
+def full_check_file(path, limit: int = 10, ranges=None, reads_to_check: int = 10, world: Optional[int] = None,
+                    device: Optional[int] = None, halo: int = 2 << 20, coll_device=None,
+                    records_path: Optional[str] = None, split_size: int = 2 << 20):
+    """`full-check` over byte-range shards (FullCheck.scala:88-323 with Blocks' partitions, Blocks.scala:141-207).
+    Each shard full-checks the blocks it owns and samples its first `limit` close calls of keys 1 and 2 (and its
+    disagreements with the `.records` truth) as PosMetadata lines — the next record of a sampled position may lie in
+    the halo, which grows when needed.  In a process group (RCCL on GPUs) rank 0 reads the header and broadcasts the
+    contig lengths (device tensor) and names; the Counts meet in one all_reduce on `coll_device` (reduceByKey,
+    FullCheck.scala:160-168) and the sampled lines in one all_gather_object (the driver's take(limit)).  Without a
+    process group, `world` shards run one after another on `device` (a file larger than HBM in windows).
+    Returns the merged sbam.cli.FullCheckParts on every rank."""
+    import sbam
+    from sbam.cli import FullCheckParts, FullCheckReport, merge_parts
+    source, size = file_source(path) if isinstance(path, (str, os.PathLike)) else path
+    grouped = _dist_ready()  # in a process group the collectives run even at world size 1 (RCCL exercised)
+    if grouped:
+        import torch.distributed as dist
+        world, rank = dist.get_world_size(), dist.get_rank()
+        ranks = [rank]
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", 0))
+    else:
+        world, rank = world or 1, 0
+        ranks = list(range(world))
+        device = 0 if device is None else device
+    lens, names = read_header_names(source, size, device) if rank == 0 else (None, None)
+    if grouped:
+        import torch.distributed as dist
+        lens = broadcast_lengths(lens, coll_device)
+        box = [names]
+        dist.broadcast_object_list(box, src=0, device=coll_device)
+        names = box[0]
+    plans = plan_shards(size, split_size, world)
+    parts = []
+    for r in ranks:
+        sh = GpuShard(plans[r], source, split_size, lens, device=device, halo=halo, reads_to_check=reads_to_check)
+        try:
+            parts.append(sh.run_with(lambda f, p: FullCheckReport(
+                f, None, records_path, limit, ranges, reads_to_check, blocks=owned_blocks(f, p),
+                names=names).parts()))
+        finally:
+            sh.close()
+    if grouped:
+        import torch
+        import torch.distributed as dist
+        mine = parts[0]
+        c = torch.from_numpy(_pack_parts_counts(mine))
+        if coll_device is not None:
+            c = c.to(coll_device)
+        dist.all_reduce(c, op=dist.ReduceOp.SUM)
+        v = c.cpu().numpy()
+        lists = [None] * world
+        dist.all_gather_object(lists, (mine.close, mine.truth))
+        o = 0
+        fields = []
+        for n, shape in ((19, (19,)), (21 * 19, (21, 19)), (21, (21,)), (21 * 128, (21, 128)), (19 * 19, (19, 19))):
+            fields.append(v[o:o + n].reshape(shape))
+            o += n
+        parts = [FullCheckParts(*fields, int(v[o]), int(v[o + 1]), close, truth) if i == 0 else
+                 FullCheckParts(*(np.zeros_like(x) for x in fields), 0, 0, close, truth)
+                 for i, (close, truth) in enumerate(lists)]
+    return merge_parts(parts, limit)
 
 
 class WindowPipe:
@@ -393,12 +502,19 @@ class WindowPipe:
         if (lo, hi) != self._range(w):  # the context's halo grew since staging: stage again
             lo, hi = self._range(w)
             buf = self.stage(lo, hi, k)
+        src = self._source(lo, hi, buf)
         if self.ctx[j] is None:
-            self.ctx[j] = GpuShard(wp, lambda a, b: buf if (a, b) == (lo, hi) else self.stage(a, b, k),
-                                   self.split_size, self.contig_lengths, device=self.device, halo=self.halo)
+            self.ctx[j] = GpuShard(wp, src, self.split_size, self.contig_lengths, device=self.device, halo=self.halo)
         else:
-            self.ctx[j].reload(wp, buf)
+            self.ctx[j].reload(wp, buf, src)
         return self.ctx[j]
+
+    def _source(self, lo, hi, buf):
+        """The byte source of one loaded window: its staged bytes for its own range; any other range (a halo retry)
+        is staged into a private buffer, never into a shared staging slot."""
+        def src(a, b):
+            return buf if (a, b) == (lo, hi) else self.stage(a, b, None)
+        return src
 
     def step(self) -> list:
         W = len(self.wplans)

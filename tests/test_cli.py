@@ -47,6 +47,7 @@ class OracleBam:
         import oracle
         self.o = oracle.BamFile(data)
         self.uncompressed_size = self.o.L
+        self.loads_to_eof = True
 
     def blocks(self):
         return self.o.start, self.o.csize, self.o.usize, self.o.uoff[:-1]
@@ -213,3 +214,43 @@ def test_cli_sharded_ranks_match_single(tmp_path, cmd):
                    timeout=100)
     a, b = one.read_text().split("\n"), two.read_text().split("\n")
     assert a[1:] == b[1:] and len(a) > 3
+
+
+@pytest.mark.parametrize("golden,bam,args", CASES)
+def test_full_check_parts_merge_in_file_order(golden, bam, args):
+    """full-check --gpus N / --windows W assemble the report from per-shard parts (sbam.cli.merge_parts): Counts
+    summed, the sampled close calls and the truth comparison concatenated in file order and cut to the limit.  The
+    blocks split into three contiguous shards on the oracle backend give every golden verbatim."""
+    import numpy as np
+    from sbam import cli
+    data = open(os.path.join(FIXTURES, bam), "rb").read()
+    ranges = cli.parse_ranges(args[args.index("-i") + 1]) if "-i" in args else None
+    records = os.path.join(FIXTURES, bam + ".records") if golden != "1.noblocks.bam" else None
+    ob = OracleBam(data)
+    nb = ob.blocks()[0].size
+    parts = []
+    for a, b in ((0, nb // 3), (nb // 3, 2 * nb // 3), (2 * nb // 3, nb)):
+        m = np.zeros(nb, bool)
+        m[a:b] = True
+        parts.append(cli.FullCheckReport(ob, data, records, 10, ranges, blocks=m).parts())
+    merged = cli.merge_parts(parts, 10)
+    assert "\n".join(cli.full_check_lines(merged, 10)) + "\n" == open(os.path.join(GOLDEN, "full-check", golden)).read()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("golden,bam,args", [CASES[0], CASES[4], CASES[5]])
+@pytest.mark.parametrize("mode", [["--gpus", "2", "--dist-backend", "gloo", "--device", "0"], ["--windows", "3"]])
+def test_full_check_sharded_matches_golden(tmp_path, golden, bam, args, mode):
+    """full-check over byte-range shards (sbam.dist.full_check_file): two ranks (torch.distributed.run; gloo on GPU 0
+    to rehearse on one card) or three windows one after another on one GPU — the report equals the golden."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    path = tmp_path / bam
+    shutil.copy(os.path.join(FIXTURES, bam), path)
+    shutil.copy(os.path.join(FIXTURES, bam + ".records"), str(path) + ".records")
+    out = tmp_path / "out.txt"
+    env = dict(os.environ, PYTHONPATH=os.path.join(ROOT, "spark-bam_amd"))
+    subprocess.run([sys.executable, "-m", "sbam.cli", "full-check", "-l", "10", *args, *mode, str(path), str(out)],
+                   check=True, env=env, timeout=200)
+    assert out.read_text() == open(os.path.join(GOLDEN, "full-check", golden)).read()

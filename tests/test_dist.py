@@ -242,3 +242,50 @@ def test_run_file_gloo_world2_gpu_shards(tmp_path, name, split_size):
     splits, sizes, totals, npos, ns = _expected(name, split_size)
     for rank, sp, sz, tot, nsucc, pos in got:
         assert sp == splits and sz == sizes and tot == totals.tolist() and nsucc == ns and pos == npos.tolist()
+
+
+def _rccl_worker(port, path, split_size, golden, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        from sbam import cli
+        from sbam import dist as sdist
+        assert dist.get_backend() == "nccl"
+        lens = sdist.broadcast_lengths(np.arange(84, dtype=np.int64) * 7 + 1, dev)
+        r = sdist.run_file(path, split_size, device=0, coll_device=dev)
+        parts = sdist.full_check_file(path, 10, None, 10, device=0, coll_device=dev, records_path=path + ".records")
+        text = "\n".join(cli.full_check_lines(parts, 10)) + "\n"
+        q.put((lens.tolist(), [str(s) for s in r.splits], r.partition_sizes, r.counts["totals"].tolist(),
+               r.counts["n_success"], text == golden))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_collectives_single_rank(tmp_path):
+    """The RCCL path (backend "nccl" = RCCL on ROCm) on device tensors, in a one-rank group on GPU 0: broadcast_lengths,
+    run_file's all_gather_into_tensor + all_reduce (gather_results) and full_check_file's all_reduce,
+    all_gather_object and broadcast_object_list — the collectives the 8-GPU runs use (CanLoadBam.scala:262-271,
+    FullCheck.scala:160-168).  Results equal the single-process oracle's splits/Counts and the full-check golden."""
+    import multiprocessing as mp
+    from conftest import FIXTURES, GOLDEN
+    name, split_size = "2.bam", 100000
+    path = tmp_path / name
+    path.write_bytes(fixture_bytes(name))
+    (tmp_path / (name + ".records")).write_bytes(open(os.path.join(FIXTURES, name + ".records"), "rb").read())
+    golden = open(os.path.join(GOLDEN, "full-check", name)).read()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), str(path), split_size, golden, q))
+    p.start()
+    lens, sp, sz, tot, nsucc, golden_ok = q.get(timeout=150)
+    p.join(60)
+    assert p.exitcode == 0
+    assert lens == (np.arange(84) * 7 + 1).tolist()
+    splits, sizes, totals, npos, ns = _expected(name, split_size)
+    assert sp == splits and sz == sizes and tot == totals.tolist() and nsucc == ns
+    assert golden_ok

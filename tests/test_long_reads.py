@@ -145,3 +145,43 @@ class TestLongReadsGpu:
         assert np.array_equal(u["totals"], c.sum(0)) and np.array_equal(u["positions"], npos)
         assert u["n_success"] == ns == s.n_records
         assert grew >= 1, "no shard needed a larger halo: the test does not reach the halo path"
+
+    @pytest.mark.parametrize("windows,split_size", [(4, 256 * 1024), (6, 64 * 1024)])
+    def test_window_pipe_halo_growth_reused_buffers(self, long_file, windows, split_size):
+        """sbam.dist.WindowPipe (bench --windows) with a 64 KiB halo over long reads: contexts grow their halo and
+        re-read their range inside the pipe while the stager and loader threads reuse three staging buffers.  A halo
+        retry must read private bytes (stage(lo, hi, None)), never a shared slot: the combined result equals the
+        single-file oracle's for both steps (the second step reloads both contexts)."""
+        import oracle
+        from sbam import dist as sdist
+        s, d, o = long_file
+        bufs = [np.zeros(0, np.uint8) for _ in range(sdist.WindowPipe.NBUF)]
+
+        def stage(lo, hi, k):
+            hi = min(hi, s.size)
+            if k is None:
+                return s.slice(lo, hi)
+            if bufs[k].size < hi - lo:
+                bufs[k] = np.zeros(hi - lo, np.uint8)
+            return s.slice(lo, hi, bufs[k][:hi - lo])
+
+        wplans = sdist.plan_shards(s.size, split_size, windows)
+        pipe = sdist.WindowPipe(wplans, stage, split_size, s.contig_lengths, 0, lambda sh: sh.step(),
+                                halo=64 * 1024)
+        want, parts = oracle.compute_splits(o, split_size)
+        c, npos, rbe, ns = o.counts_parallel(0, o.L, 10, 8)
+        try:
+            for _ in range(2):
+                results = pipe.step()
+                counts = np.sum([r.counts for r in results], axis=0)
+                results = [sdist.ShardResult(counts if i == 0 else np.zeros_like(counts), r.first_block_pos,
+                                             r.first_offset, r.nonempty, r.n_records) for i, r in enumerate(results)]
+                splits, sizes, merged = sdist.combine(results, s.size)
+                assert [str(x) for x in splits] == [f"{a}-{b}" for a, b in want]
+                assert sizes == [len(q) for q in parts]
+                u = sdist.unpack_counts(merged)
+                assert np.array_equal(u["totals"], c.sum(0)) and np.array_equal(u["positions"], npos)
+                assert u["n_success"] == ns == s.n_records
+            assert any(sh.halo > 64 * 1024 for sh in pipe.ctx), "no context grew its halo inside the pipe"
+        finally:
+            pipe.close()

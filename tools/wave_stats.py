@@ -26,15 +26,15 @@ f.reset(); f.run(contig_lengths=s.contig_lengths)
 fn(buf, 1)
 v = list(buf)
 names = ["header", "build", "stage", "phaseA", "phaseB", "scanC", "rounds", "b_iters", "total", "headers",
-         "hdr_cl_setup", "hdr_chain", "hdr_stage"]
+         "hdr_cl_setup", "hdr_chain", "hdr_stage", "warmup"]
 tot = v[8]
 out = {n: v[i] for i, n in enumerate(names)}
-out.update({f"{n}_pct": round(100.0 * v[i] / tot, 1) for i, n in enumerate(names[:6])})
+out.update({f"{n}_pct": round(100.0 * v[i] / tot, 1) for i, n in list(enumerate(names[:6])) + [(13, "warmup")]})
 out["blocks"] = int(f.n_blocks)
 out["decode_ms"] = f.kernel_ms("inflate_decode")
 out["fallbacks"] = f.inflate_fallbacks()
 out["b_iters_per_round"] = round(v[7] / max(v[6], 1), 3)
 out["rounds_per_block"] = round(v[6] / out["blocks"], 3)
 out["cycles_per_header"] = {n: round(v[i] / max(v[9], 1)) for i, n in ((0, "rest"), (10, "cl_setup"), (11, "chain"), (12, "stage"), (1, "build"))}
-out["cycles_per_round"] = {n: round(v[i] / max(v[6], 1)) for i, n in enumerate(names[2:6], 2)}
+out["cycles_per_round"] = {n: round(v[i] / max(v[6], 1)) for i, n in list(enumerate(names[2:6], 2)) + [(13, "warmup")]}
 print(json.dumps(out))
