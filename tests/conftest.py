@@ -49,3 +49,15 @@ def gpu_files():
     yield get
     for f in cache.values():
         f.close()
+
+
+@pytest.fixture(scope="session")
+def distinct_synth():
+    """A multi-GB synthetic Illumina-like BAM (the bench generator) with NO repeated tile: every 64 MB tile has its
+    own seed (tools/synth.py distinct=True).  SBAM_SCALE_GB sets the size (default 4).  Shared by the at-scale tests."""
+    import synth
+    gb = float(os.environ.get("SBAM_SCALE_GB", "4"))
+    s = synth.SynthBam.for_size(int(gb * 1.01e9), tile_mb=64, threads=16, distinct=True)
+    digests = {hash(t[:1 << 16].tobytes()) for t in s.tiles[: s.copies]}
+    assert len(digests) == s.copies, "a tile repeats"
+    return s

@@ -49,10 +49,47 @@ def test_library_is_gfx950_code_object():
     assert b"gfx950" in data
 
 
-def test_load_replaces_window_on_gpu_marker():
-    """(CPU) sbam_load is declared and bound like sbam_open (GPU behaviour: test_load_window_gpu)."""
+def header_prototypes():
+    """name -> (return type, [parameter types]) for every function include/sbam.h declares."""
+    src = open(os.path.join(ROOT, "include", "sbam.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    out = {}
+    for m in re.finditer(r"([A-Za-z_][\w \*]*?)\b(sbam_[a-z_]+)\s*\(([^)]*)\)\s*;", src):
+        params = [p.strip() for p in m.group(3).split(",") if p.strip() and p.strip() != "void"]
+        out[m.group(2)] = (m.group(1).strip(), [re.sub(r"\s*\b\w+$", "", p) if not p.endswith("*") else p
+                                                for p in params])
+    return out
+
+
+def _kind(c_type: str) -> str:
+    t = c_type.replace("const", "").strip()
+    if "*" in t:
+        return "ptr"
+    return {"int64_t": "i64", "int32_t": "i32", "int": "i32", "uint32_t": "i32", "double": "f64",
+            "sbam_pos": "pos"}.get(t, t)
+
+
+def _ctypes_kind(ct) -> str:
+    import ctypes as C
     import sbam
-    assert "sbam_load" in sbam.EXPORTS
+    if ct in (C.c_void_p, C.c_char_p) or isinstance(ct, type(C.POINTER(C.c_int))):
+        return "ptr"
+    return {C.c_int64: "i64", C.c_int32: "i32", C.c_int: "i32", C.c_uint32: "i32", C.c_double: "f64",
+            sbam._Pos: "pos"}.get(ct, repr(ct))
+
+
+def test_ctypes_bindings_match_header_prototypes():
+    """Every declared function's ctypes binding has the header's arity and argument widths (i64 / i32 / pointer /
+    sbam_pos by value): a mismatch would pass wrong-width arguments silently through the C ABI."""
+    import sbam
+    L = sbam.load_library()
+    protos = header_prototypes()
+    assert sorted(protos) == header_functions()
+    for name, (ret, params) in protos.items():
+        fn = getattr(L, name)
+        want = [_kind(p) for p in params]
+        got = [_ctypes_kind(a) for a in (fn.argtypes or [])]
+        assert got == want, (name, got, want)
 
 
 import pytest  # noqa: E402

@@ -213,3 +213,28 @@ def test_sam_is_not_bam():
     sam = b"@HD\tVN:1.5\tSO:coordinate\n" * 10
     with pytest.raises(sbam.HeaderParseException, match=r"Position 0: 64 != 31"):
         sbam.BamFile(sam)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,window,kind", [("2.bam", 96 * 1024, "eager"), ("1.bam", 200 * 1024, "eager"),
+                                              ("1.2203053-2211029.bam", 128 * 1024, "full")])
+def test_lazy_block_checker_drop_in(tmp_path, name, window, kind):
+    """sbam.checker.LazyBlockChecker, the MakeChecker drop-in (Checker.scala:23-25: built from the channel alone): the
+    positions of every block in CallPartition's order (blocks.flatMap(PosIterator), CallPartition.scala:39-53) give
+    the whole-file calls; each window of blocks costs one bulk call on first use."""
+    import sbam
+    from sbam import dist as sdist
+    from sbam.checker import make_checker
+    path = tmp_path / name
+    path.write_bytes(fixture_bytes(name))
+    with sbam.BamFile(fixture_bytes(name)) as f:
+        want = f.check_eager() if kind == "eager" else f.check_full_words()
+        st, cs, us, uo = f.blocks()
+        lens = f.contig_lengths
+    chk = make_checker(lens, kind=kind, window=window)(sdist.file_source(str(path)))
+    rng = np.random.default_rng(7)
+    for b in range(st.size):
+        offs = np.arange(int(us[b])) if b % 4 == 0 else np.sort(rng.integers(0, int(us[b]), 200))
+        got = [chk(sbam.Pos(int(st[b]), int(o))) for o in offs]
+        assert got == [bool(want[uo[b] + o]) if kind == "eager" else int(want[uo[b] + o]) for o in offs], b
+    assert 1 < chk.bulk_calls < st.size

@@ -2,7 +2,8 @@
 result word at every offset of randomly sampled block runs equals the CPU oracle's, the oracle inflating those
 blocks itself from the compressed bytes (an independent stream); 4096 sampled blocks inflate to the CRC32 and
 ISIZE their BGZF footers store; and the eager and full checks agree at every offset and call exactly the
-generated records.  SBAM_SCALE_GB sets the size (default 4)."""
+generated records.  The file has no repeated tile (conftest.distinct_synth); SBAM_SCALE_GB sets the size (default
+4)."""
 import os
 
 import numpy as np
@@ -12,17 +13,19 @@ GB = float(os.environ.get("SBAM_SCALE_GB", "4"))
 
 
 @pytest.mark.gpu
-def test_sampled_verdicts_at_scale():
+@pytest.mark.timeout(600)
+def test_sampled_verdicts_at_scale(distinct_synth):
     import oracle
     import sbam
-    import synth
-    s = synth.SynthBam.for_size(int(GB * 1e9), tile_mb=64, threads=16)
+    s = distinct_synth  # no repeated tile: the 48 sampled runs come from different tiles
     data = s.bytes()
     lens = np.asarray(s.contig_lengths, np.int64)
     with sbam.BamFile(data, path="synth.bam") as g:
         st, cs, us, uo = g.blocks()
         rng = np.random.default_rng(0x5EED)
         picks = np.sort(rng.choice(st.size - 40, 48, replace=False))
+        tiles = {int(np.searchsorted(s.tile_starts, int(st[b]), side="right")) for b in picks.tolist()}
+        assert len(tiles) >= 24, "samples concentrated in few tiles"
         compared = 0
         for b in picks.tolist():
             # 24 whole blocks as an independent BGZF stream; positions of the first 8 are compared (their

@@ -45,13 +45,23 @@ def _take(p, n) -> np.ndarray:
     return a
 
 
+def tile_seed(seed: int, k: int) -> int:
+    """Seed of tile k of a distinct-tile file (tile 0 keeps `seed`)."""
+    return (seed + k * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+
+
 class SynthBam:
+    """`distinct=False`: one tile repeated `copies` times (the bench input: any byte range is cheap to produce).
+    `distinct=True`: `copies` different tiles (tile k from tile_seed(seed, k), generated in parallel), so a multi-GB
+    file has no repeated tile — the large-size parity tests compare it with full oracle runs."""
+
     def __init__(self, tile_mb: float = 64.0, copies: int = 1, read_len: int = 150, seed: int = 0x5EEDBA11,
-                 level: int = 6, threads: int = 16, unplaced_mb: float | None = None):
+                 level: int = 6, threads: int = 16, unplaced_mb: float | None = None, distinct: bool = False):
         L = lib()
         p = ctypes.c_void_p()
         n = L.synth_header(ctypes.byref(p))
         self.header = _take(p, n)
+        self.seed, self.read_len, self.level, self.tile_mb, self.threads = seed, read_len, level, tile_mb, threads
         nrec, ulen = ctypes.c_int64(0), ctypes.c_int64(0)
         n = L.synth_tile(seed, int(tile_mb * 3 * 2 ** 20), read_len, level, threads, ctypes.byref(p),
                          ctypes.byref(nrec), ctypes.byref(ulen))
@@ -68,24 +78,55 @@ class SynthBam:
                                  ctypes.byref(nrec), ctypes.byref(ulen))
             self.tail = _take(p, n)
             self.tail_records = nrec.value
+        self.distinct = distinct
+        self.tiles = [self.tile]
+        self.tiles_records = [self.tile_records]
         self.copies = copies
+        if distinct:
+            self._make_tiles(copies)
         self._sizes()
         nr = ctypes.c_int32(0)
         lens = np.zeros(128, np.int64)
         L.synth_contigs(ctypes.byref(nr), lens.ctypes.data)
         self.contig_lengths = lens[: nr.value]
 
+    def _make_tiles(self, k: int):
+        """Tiles 1 .. k-1 of a distinct-tile file, one generator call per worker thread (ctypes releases the GIL)."""
+        from concurrent.futures import ThreadPoolExecutor
+        L = lib()
+
+        def one(i):
+            p = ctypes.c_void_p()
+            nrec, ulen = ctypes.c_int64(0), ctypes.c_int64(0)
+            n = L.synth_tile(tile_seed(self.seed, i), int(self.tile_mb * 3 * 2 ** 20), self.read_len, self.level, 1,
+                             ctypes.byref(p), ctypes.byref(nrec), ctypes.byref(ulen))
+            return _take(p, n), nrec.value
+        with ThreadPoolExecutor(self.threads) as ex:
+            got = list(ex.map(one, range(len(self.tiles), k)))
+        self.tiles += [t for t, _ in got]
+        self.tiles_records += [r for _, r in got]
+
     @staticmethod
     def for_size(target_bytes: int, tile_mb: float = 64.0, **kw) -> "SynthBam":
+        distinct = kw.pop("distinct", False)
         s = SynthBam(tile_mb=tile_mb, copies=1, **kw)
         s.copies = max(1, round((target_bytes - s.header.size - s.tail.size - 28) / s.tile.size))
+        if distinct:
+            s.distinct = True
+            s._make_tiles(s.copies)
         s._sizes()
         return s
 
     def _sizes(self):
-        self.body = self.header.size + self.copies * self.tile.size  # where the unplaced tail starts
+        if self.distinct:
+            sz = np.array([t.size for t in self.tiles[: self.copies]], np.int64)
+            self.tile_starts = self.header.size + np.concatenate([[0], np.cumsum(sz)])
+            self.body = int(self.tile_starts[-1])
+            self.n_records = int(sum(self.tiles_records[: self.copies])) + self.tail_records
+        else:
+            self.body = self.header.size + self.copies * self.tile.size  # where the unplaced tail starts
+            self.n_records = self.copies * self.tile_records + self.tail_records
         self.size = self.body + self.tail.size + 28
-        self.n_records = self.copies * self.tile_records + self.tail_records
 
     def slice(self, lo: int, hi: int, out: np.ndarray | None = None) -> np.ndarray:
         """File bytes [lo, hi) (hi clamped to the file size)."""
@@ -98,9 +139,14 @@ class SynthBam:
                 n = min(hi, H) - pos
                 out[pos - lo: pos - lo + n] = self.header[pos: pos + n]
             elif pos < self.body:
-                k, o = divmod(pos - H, T)
-                n = min(hi - pos, T - o)
-                out[pos - lo: pos - lo + n] = self.tile[o: o + n]
+                if self.distinct:
+                    k = int(np.searchsorted(self.tile_starts, pos, side="right")) - 1
+                    tile, o = self.tiles[k], pos - int(self.tile_starts[k])
+                else:
+                    k, o = divmod(pos - H, T)
+                    tile = self.tile
+                n = min(hi - pos, tile.size - o)
+                out[pos - lo: pos - lo + n] = tile[o: o + n]
             elif pos < self.body + self.tail.size:
                 o = pos - self.body
                 n = min(hi - pos, self.tail.size - o)
