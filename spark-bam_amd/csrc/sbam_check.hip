@@ -641,6 +641,36 @@ SB_DEV void stage_tile(const StreamView &sv, int64_t base, uint8_t *s_win, uint3
   if (threadIdx.x < 16) s_opc[kWin / 32 + threadIdx.x] = 0;  // the 4 pad words of every class
 }
 
+// Per window byte c < kFbBytes: fb[c] = index of the first invalid CIGAR op among the ops at c, c + 4, ... (exact
+// below 64; >= 64 means none among the first 64), so that a position's CIGAR test is one LDS byte read.  Thread i
+// covers bytes [32 i, 32 i + 32), the 8 ops of each residue class there: the value just past the chunk comes from
+// the op-class bitmap (ctz of 64 bits, capped at 64), then F_j = bad(op j) ? 0 : F_(j+1) + 1 runs backward over the
+// chunk's 8 dwords, all four classes at once (one byte each).  Needs stage_tile's bitmaps (a barrier between).
+constexpr int kFbBytes = ((kTile + 36 + 255 + 31) / 32) * 32;
+SB_DEV void stage_fb(const uint8_t *s_win, const uint32_t *s_opc, uint8_t *s_fb) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  for (int i = threadIdx.x; i < kFbBytes / 32; i += kCheckThreads) {
+    uint32_t F = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const uint64_t om = op_bits(s_opc, 32 * i + 32 + r);
+      const uint32_t z = om ? (uint32_t)__builtin_ctzll(om) : 64u;
+      F |= z << (8 * r);
+    }
+    const u32x4 a = reinterpret_cast<const u32x4 *>(s_win)[2 * i], b = reinterpret_cast<const u32x4 *>(s_win)[2 * i + 1];
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint32_t o[8];
+#pragma unroll
+    for (int j = 7; j >= 0; j--) {
+      const uint32_t bad = (((w[j] & 0x0f0f0f0fu) + 0x07070707u) >> 4) & 0x01010101u;  // (b & 0xf) > 8, bit 0
+      F = (F + 0x01010101u) & ~((bad << 8) - bad);  // bad bytes -> 0xff
+      o[j] = F;
+    }
+    reinterpret_cast<u32x4 *>(s_fb)[2 * i] = u32x4{o[0], o[1], o[2], o[3]};
+    reinterpret_cast<u32x4 *>(s_fb)[2 * i + 1] = u32x4{o[4], o[5], o[6], o[7]};
+  }
+}
+
 // ---- the tiled kernel -------------------------------------------------------------------------------------
 enum { MODE_COUNTS = 0, MODE_EAGER = 1, MODE_WORDS = 2, MODE_BYKEY = 3 };
 
@@ -1035,6 +1065,7 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bi
   __shared__ __attribute__((aligned(16))) uint8_t s_win[kWin + 64];
   __shared__ uint32_t s_opc[4 * kOpcWords];
   __shared__ uint32_t s_nbad[kNameWords];
+  __shared__ __attribute__((aligned(16))) uint8_t s_fb[kFbBytes];  // first invalid op from each byte (stage_fb)
   __shared__ uint32_t s_pl[3][kCheckThreads + 8];  // per lane: I < -1, I >= n_ref, 0 <= I < n_ref && I(+4) > len[I]
   __shared__ unsigned long long s_acc[19 + 21];     // totals, positions per key
   __shared__ uint32_t s_k12[3 * 19];
@@ -1071,6 +1102,7 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bi
     __syncthreads();
     stage_tile(sv, base, s_win, s_opc, s_nbad);
     __syncthreads();
+    stage_fb(s_win, s_opc, s_fb);
     // ---- predicate pass over the offsets 1024 j + 4 t + o; lanes t < 8 add row 8 (offsets 8192 + 4 t + o), which
     // shifts row 0 out and leaves exactly the planes of lanes 256 + t
     {
@@ -1120,11 +1152,10 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bi
         const int32_t nc = (int32_t)(fld(4) & 0xffffu);
         const int32_t ls = (int32_t)fld(5);
         const uint32_t last = s_win[rel + 35 + lrn];  // the name's last byte (read for lrn < 2 too, unused then)
-        // first invalid op (0xffffffff: none among the 64 one bitmap read covers)
-        const uint64_t om = op_bits(s_opc, rel + 36 + (lrn >= 2 ? lrn : 0));
-        const uint32_t obad = ctz64((uint32_t)om, (uint32_t)(om >> 32));
+        // first invalid op (>= 64: none among the first 64)
+        const uint32_t obad = s_fb[rel + 36 + (lrn >= 2 ? lrn : 0)];
         pLZ = push_bit(pLZ, last == 0);
-        pIV = push_bit(pIV, obad < (uint32_t)nc);  // an invalid op among the first min(nc, 64)
+        pIV = push_bit(pIV, obad < min((uint32_t)nc, 64u));  // an invalid op among the first min(nc, 64)
         pTF = push_bit(pTF, too_few_remaining(bs, lrn, nc, ls));
         pNG = push_bit(pNG, nc > 64);  // op array past the 64 checked ops
         pZ = push_bit(pZ, lrn == 0);

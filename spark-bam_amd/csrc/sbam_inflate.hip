@@ -699,6 +699,9 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
   }
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));  // 16-B store at a 4-B aligned address
+
 // ---- wave decoder (fast path) -------------------------------------------------------------------------------
 // One wavefront per BGZF block.  Huffman decoding is serial per stream, so the 64 lanes decode 64 consecutive
 // kK-bit segments of a deflate block's data at once, each from a guessed start (its segment's first bit, in the
@@ -739,6 +742,14 @@ constexpr int kCpSteps = 8;        // symbols between checkpoints
 // no warm-up 79.5 ms; 128 bits 74.8; 256: 71.6; 384: 69.6; 512 (one segment; lane 1 from the round's true start):
 // 68.5; 640: 70.1; 1024: 76.7.
 constexpr int kWarm = kK;
+// Phase A keeps the tokens of its first kTR symbol steps in registers (two per VGPR, step j in half j & 1 of
+// tr[j / 2]: the steps are unrolled, so every index is static).  A lane whose phase-A path is the true one (the
+// common case after the warm-up) then only stores them in phase C; it decodes again only past step kTR.
+#ifndef SBAM_TR
+#define SBAM_TR 96
+#endif
+constexpr int kTR = SBAM_TR;
+static_assert(kTR % 2 == 0 && kTR <= kCp * kCpSteps, "register tokens come from the unrolled checkpoint steps");
 constexpr int kScratchDw = 256;    // window tail that doubles as header / table-build scratch
 constexpr uint32_t kSub = 1u << 10;  // table entry flag: pointer to a sub-table
 // a block header (<= 3 + 14 + 57 + 320 * 14 bits) plus the window's start alignment fits before the scratch
@@ -748,8 +759,9 @@ enum : int { ST_NONE = 0, ST_EOB = 1, ST_ERR = 2, ST_OUT = 3 };
 }  // namespace wd
 
 // Table entry (u32): bits 0-3 code length, 4-7 extra bits, 8-9 kind, 10 sub-table flag, 11-15 sub-table index
-// bits, 16-31 value (literal byte, length or distance base; K_SPEC: 0 = end of block, 1 = invalid symbol; for a
-// sub-table pointer: the sub-table's offset in the alphabet's table).
+// bits, 16-31 value in token form, so that value + extra bits is the symbol's u16 token (literal byte; 253 + length
+// base; 0x7fff + distance base; K_SPEC: 0 = end of block, 1 = invalid symbol; for a sub-table pointer: the
+// sub-table's offset in the alphabet's table).
 struct WaveLds {
   uint32_t win[wd::kWinDw];
   uint32_t tab[wd::kTab];
@@ -778,14 +790,14 @@ SB_DEV uint32_t sym_entry(uint32_t s, uint32_t l, bool dist) {
       const uint32_t k = s - 257;
       const uint32_t x = (k < 8 || k == 28) ? 0u : (k >> 2) - 1;
       const uint32_t base = k < 8 ? k + 3 : k == 28 ? 258u : ((4u | (k & 3)) << x) + 3;
-      return l | (x << 4) | (K_LEN << 8) | (base << 16);
+      return l | (x << 4) | (K_LEN << 8) | ((base + 253u) << 16);  // token form: 253 + length
     }
     return l | (K_SPEC << 8) | (1u << 16);
   }
   if (s < 30) {
     const uint32_t x = s < 4 ? 0u : (s >> 1) - 1;
     const uint32_t base = s < 4 ? s + 1 : ((2u | (s & 1)) << x) + 1;
-    return l | (x << 4) | (K_DIST << 8) | (base << 16);
+    return l | (x << 4) | (K_DIST << 8) | ((base + 0x7fffu) << 16);  // token form: kTokDist | (distance - 1)
   }
   return l | (K_SPEC << 8) | (1u << 16);
 }
@@ -915,7 +927,7 @@ SB_DEV bool wave_build(WaveLds &L, int off, int nsym, int toff, int subcap) {
 // One symbol of the alphabet `st` selects (literal/length, or distance after a length) at bit position pos of the
 // staged window (positions are bits from the block's 16-B aligned base; wq = the window's first bit): 32 bits of
 // lookahead from two window dwords, the root entry, the sub-table entry for long codes, the extra bits.  Advances
-// pos; returns the entry, v = literal byte, length, distance or K_SPEC value.
+// pos; returns the entry, v = the symbol's token (literal byte, 253 + length, 0x7fff + distance) or K_SPEC value.
 SB_DEV uint32_t wsym(const WaveLds &L, int wq, int &pos, int st, uint32_t &v) {
   using namespace wd;
   const uint32_t q = (uint32_t)(pos - wq), w = q >> 5;
@@ -982,13 +994,14 @@ struct SegResult {
 };
 
 #ifdef SBAM_WAVE_STATS
-__device__ unsigned long long g_wave_stats[16];
+constexpr int kWaveStats = 32;
+__device__ unsigned long long g_wave_stats[kWaveStats];
 #define WMARK(slot) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); ws_[slot] += t_ - wt_; wt_ = t_; } while (0)
 #define WADD(slot, v) ws_[slot] += (v)
 extern "C" int sbam_debug_wave_stats(unsigned long long *out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_stats), sizeof(g_wave_stats)) != hipSuccess) return -1;
   if (reset) {
-    static const unsigned long long z[16] = {0};
+    static const unsigned long long z[kWaveStats] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_wave_stats), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;
@@ -1028,7 +1041,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
   int out = 0, ntok = 0;
   bool ok = true;
 #ifdef SBAM_WAVE_STATS
-  uint64_t ws_[16] = {0};
+  uint64_t ws_[kWaveStats] = {0};
   uint64_t wt_ = __builtin_amdgcn_s_memtime();
   const uint64_t wt0_ = wt_;
 #endif
@@ -1197,6 +1210,9 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       uint32_t s1p = ~0u, s1e = 0, s1c = 0, s2p = ~0u, s2e = 0, s2c = 0;  // stops: start, exit | kind, counts
       int nst = 0;
       uint32_t tokA = 0, bytA = 0, exitEnd, entry;
+      uint32_t tr[kTR / 2];  // phase-A tokens of steps [0, kTR)
+      uint32_t stR = 0, bytR = 0;  // state (exit key) and bytes after step kTR
+      int slack = 1 << 30;  // min over the phase-A path's distances of (local bytes before the match - distance)
       {
         int stt = lane == 0 ? (int)((S >> 9) & 1) : 0;
         uint32_t pl = lane == 0 ? (S & 511u) : 0u;
@@ -1217,7 +1233,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
           while (rp < seg_start) {
             uint32_t v;
             const uint32_t kind = (wsym(L, wq, rp, stt, v) >> 8) & 3u;
-            pl = kind == K_LEN ? v : pl;
+            pl = kind == K_LEN ? v - 253u : pl;
             stt = kind == K_LEN ? 1 : 0;
           }
         }
@@ -1225,7 +1241,9 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         entry = ((uint32_t)rp << 10) | ((uint32_t)stt << 9) | pl;
         // one symbol, predicated: a lane that is done (stopped out of the data, or past its segment) decodes the
         // same symbol again and commits nothing, so the steps need no exec-mask branches
-        auto step = [&]() {
+        // ST: the step's index when it is below kTR (its token goes to tr), else -1
+        auto step = [&](auto ST) {
+          constexpr int sj = decltype(ST)::value;
           const bool live = go && rp < seg_end;
           const uint32_t p0 = (uint32_t)rp;
           int rq = rp;
@@ -1248,10 +1266,26 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
           }
           rp = live ? rq : rp;
           const bool cnt = live && !stp;
-          tokA += cnt ? 1u : 0u;
-          bytA += cnt ? (kind == K_LIT ? 1u : kind == K_LEN ? v : 0u) : 0u;
-          pl = (cnt && kind == K_LEN) ? v : pl;
-          stt = live ? ((cnt && kind == K_LEN) ? 1 : 0) : stt;
+          if constexpr (sj >= 0) {  // the token (a committed step j is token j of the path: no stop before it)
+            if constexpr ((sj & 1) == 0) {
+              tr[sj / 2] = v;
+            } else {
+              tr[sj / 2] = __builtin_amdgcn_perm(v, tr[sj / 2], 0x05040100u);  // low half kept, v above
+            }
+          }
+          // selects only (no exec-mask branches): counts, pending length, and the path's distance check (zlib
+          // "invalid distance too far back") up to its first stop
+          const uint32_t cm = cnt ? ~0u : 0u;  // used by every lane (a select on cnt becomes a branch)
+          const bool isLen = kind == K_LEN;
+          const uint32_t lenv = v - 253u;
+          const uint32_t nb = kind == K_LIT ? 1u : (isLen ? lenv : 0u);
+          const int sx = (int)bytA - (int)pl - (int)(v - 0x7fffu);
+          const int sv = (int)((cm & (uint32_t)sx) | (~cm & (1u << 30)));  // v_bfi
+          slack = min(slack, (nst == 0 && kind == K_DIST) ? sv : (1 << 30));
+          tokA -= cm;
+          bytA += nb & cm;
+          pl = (isLen & cnt) ? lenv : pl;
+          stt = live ? (int)(cnt & isLen) : stt;
         };
         // checkpoints every kCpSteps steps (wave-uniform, so a record costs no divergent branch): the lane's
         // position if it is at a literal/length boundary
@@ -1261,11 +1295,22 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
           cp[jj] = (live && stt == 0) ? (uint32_t)rp : ~0u;
           cc[jj] = tokA | (bytA << 12);
           if (__ballot(live) != 0) {
+            if constexpr (jj * kCpSteps < kTR) {
+              sfor<0, kCpSteps>([&](auto K) {
+                constexpr int sj = jj * kCpSteps + decltype(K)::value;
+                step(std::integral_constant<int, (sj < kTR ? sj : -1)>{});
+              });
+            } else {
 #pragma unroll 2  // (4 and 8: the same; 1: +0.5 ms)
-            for (int k = 0; k < kCpSteps; k++) step();
+              for (int k = 0; k < kCpSteps; k++) step(std::integral_constant<int, -1>{});
+            }
+          }
+          if constexpr ((jj + 1) * kCpSteps == kTR) {
+            stR = ((uint32_t)rp << 10) | ((uint32_t)stt << 9) | pl;
+            bytR = bytA;
           }
         });
-        while (__ballot(go && rp < seg_end) != 0) step();
+        while (__ballot(go && rp < seg_end) != 0) step(std::integral_constant<int, -1>{});
         exitEnd = ((uint32_t)rp << 10) | ((uint32_t)stt << 9) | pl;
       }
       WMARK(3);
@@ -1277,6 +1322,12 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       uint32_t nxt = lane == 0 ? own.exit : exitEnd;  // what the right neighbour starts from (provisional)
       uint32_t bst = lane == 0 ? S : entry;
       bool ver = lane == 0;
+      // where phase C finds the lane's tokens: kModeA — res is phase A's own result (tokens in tr from step 0);
+      // kModeR — re-decoded from the true start up to phase A's checkpoint rjP (rjtk tokens, rjby bytes), then
+      // phase A's path from step rjs (rjcb: phase A's bytes at the checkpoint); kModeF — re-decoded to the end
+      enum : int { kModeA = 0, kModeR = 1, kModeF = 2 };
+      int mode = kModeA;
+      uint32_t rjP = 0, rjs = 0, rjtk = 0, rjby = 0, rjcb = 0;
       int f = 64;
       for (;;) {
         uint32_t pex = __shfl_up(nxt, 1);
@@ -1287,6 +1338,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
           upd = nxt != own.exit;
           nxt = own.exit;
           res = own;
+          mode = kModeA;
         }
         const uint64_t vs = __ballot(ver && res.stop != ST_NONE);
         f = uni(vs ? __ffsll((unsigned long long)vs) - 1 : 64);
@@ -1307,11 +1359,22 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
             return m;
           };
           uint32_t tcp = next_cp((uint32_t)rp);
+          mode = kModeF;
           for (;;) {
             if (stt == 0 && (uint32_t)rp == tcp) {  // on the first-pass path from here
-              uint32_t cj = 0;
-              sfor<0, kCp>([&](auto I) { cj = cp[decltype(I)::value] == tcp ? cc[decltype(I)::value] : cj; });
+              uint32_t cj = 0, sj = 0;
+              sfor<0, kCp>([&](auto I) {
+                const bool hit = cp[decltype(I)::value] == tcp;
+                cj = hit ? cc[decltype(I)::value] : cj;
+                sj = hit ? (uint32_t)(decltype(I)::value * kCpSteps) : sj;
+              });
               const uint32_t P = tcp;
+              mode = kModeR;
+              rjP = P;
+              rjs = sj;
+              rjtk = tk;
+              rjby = by;
+              rjcb = cj >> 12;
               // the first recorded stop at or after the checkpoint ends the path
               const bool h1 = nst >= 1 && s1p >= P, h2 = !h1 && nst >= 2 && s2p >= P;
               if (h1 || h2) {
@@ -1325,6 +1388,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
                 break;
               }
               tcp = ~0u;  // more stops than recorded, the first after P unknown: decode the rest here
+              mode = kModeF;
             }
             if (rp >= seg_end) {
               res = SegResult{tk, by, ((uint32_t)rp << 10) | ((uint32_t)stt << 9) | pl, ST_NONE, false};
@@ -1338,8 +1402,8 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
               break;
             }
             tk++;
-            by += kind == K_LIT ? 1u : kind == K_LEN ? v : 0u;
-            pl = kind == K_LEN ? v : pl;
+            by += kind == K_LIT ? 1u : kind == K_LEN ? v - 253u : 0u;
+            pl = kind == K_LEN ? v - 253u : pl;
             stt = kind == K_LEN ? 1 : 0;
             if ((uint32_t)rp > tcp) tcp = next_cp((uint32_t)rp);
           }
@@ -1351,6 +1415,21 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       WMARK(4);
       // lanes 0..f carry the true path (f: the lane whose segment ends the deflate block, or 64)
       const bool act = lane <= f;
+#ifdef SBAM_WAVE_STATS
+      {  // token statistics of the true segments: how many lanes, how many re-decoded (phase B), token counts
+        const bool viaB = act && mode != kModeA;
+        WADD(23, __ballot(act && mode == kModeF) != 0 ? 1 : 0);
+        WADD(14, __popcll(__ballot(act)));
+        WADD(15, __popcll(__ballot(viaB)));
+        WADD(16, __popcll(__ballot(act && res.tok > 64)));
+        WADD(17, __popcll(__ballot(act && res.tok > 96)));
+        WADD(18, __popcll(__ballot(act && res.tok > 128)));
+        WADD(19, __ballot(viaB) != 0 ? 1 : 0);
+        WADD(20, __ballot(act && res.tok > 96) != 0 ? 1 : 0);
+        WADD(21, __ballot(act && res.tok > 64) != 0 ? 1 : 0);
+        WADD(22, __ballot(act && own.stop != ST_NONE) != 0 ? 1 : 0);
+      }
+#endif
       const uint32_t my_tok = act ? res.tok : 0u, my_byt = act ? res.byt : 0u;
       const uint32_t itok = wave_incl_scan(my_tok), ibyt = wave_incl_scan(my_byt);
       const uint32_t tot_tok = uni((uint32_t)__shfl(itok, 63)), tot_byt = uni((uint32_t)__shfl(ibyt, 63));
@@ -1359,30 +1438,98 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         ok = false;
         break;
       }
-      // ---- phase C: decode the true segments again, writing tokens at their offsets
+      // ---- phase C: write the true segments' tokens at their offsets.  A lane re-decodes only what phase A's
+      // registers do not hold: mode F its whole segment, mode R the stretch up to its rejoin checkpoint; then the
+      // register tokens; then whatever lies past step kTR.
       bool derr = false;
       if (act) {
         uint32_t start = __shfl_up(nxt, 1);
         if (lane == 0) start = S;
-        int stt = (int)((start >> 9) & 1);
-        uint32_t pl = start & 511u;
-        int rp = (int)(start >> 10);
-        int o = out + (int)(ibyt - my_byt);
+        const int o0 = out + (int)(ibyt - my_byt);
+        int o = o0;
         uint32_t ti = (uint32_t)ntok + (itok - my_tok);
-        while (rp < seg_end) {
-          uint32_t v;
-          const uint32_t kind = (wsym(L, wq, rp, stt, v) >> 8) & 3u;
-          if (kind == K_SPEC) break;  // the end-of-block symbol of lane f
-          const uint32_t t = kind == K_LIT ? v : kind == K_LEN ? v + 253u : kTokDist | (v - 1u);
-          if (kind == K_DIST) derr |= (int)v > o - (int)pl;
-          o += kind == K_LIT ? 1 : kind == K_LEN ? (int)v : 0;
-          pl = kind == K_LEN ? v : pl;
-          stt = kind == K_LEN ? 1 : 0;
-          *reinterpret_cast<uint16_t *>(reg + 2 * ti) = (uint16_t)t;
-          ti++;
+        // decode from key st until the reader reaches endp (or the end-of-block symbol of lane f), writing tokens
+        auto run = [&](uint32_t st, int endp) {
+          int stt = (int)((st >> 9) & 1);
+          uint32_t pl = st & 511u;
+          int rp = (int)(st >> 10);
+          while (rp < endp) {
+            uint32_t v;
+            const uint32_t kind = (wsym(L, wq, rp, stt, v) >> 8) & 3u;
+            if (kind == K_SPEC) break;
+            if (kind == K_DIST) derr |= (int)(v - 0x7fffu) > o - (int)pl;  // v: the token
+            o += kind == K_LIT ? 1 : kind == K_LEN ? (int)v - 253 : 0;
+            pl = kind == K_LEN ? v - 253u : pl;
+            stt = kind == K_LEN ? 1 : 0;
+            *reinterpret_cast<uint16_t *>(reg + 2 * ti) = (uint16_t)v;
+            ti++;
+          }
+        };
+        WMARK(24);
+        run(start, mode == kModeF ? seg_end : mode == kModeR ? (int)rjP : 0);
+        WMARK(25);
+        // register tokens [lo, hi) of phase A's path
+        const uint32_t lo = mode == kModeR ? rjs : 0u;
+        const uint32_t n = mode == kModeA ? res.tok : mode == kModeR ? res.tok - rjtk : 0u;
+        const uint32_t hi = min(lo + n, (uint32_t)kTR);
+        uint16_t *dst = reinterpret_cast<uint16_t *>(reg) + ti - lo;
+        derr |= mode == kModeA && o0 + slack < 0;  // the path's distances, checked as phase A went
+        {
+          // mode A: register tokens [0, hi) at token index ti, as 16-B stores (4-B aligned: a 2-B head when ti is
+          // odd), then 4-B and a last 2-B store — a lane's run is contiguous, so 8 tokens per store instruction
+          // instead of one (every store instruction writes 64 lanes' separate lines)
+          const uint32_t na = mode == kModeA ? hi : 0u;
+          const uint32_t par = ti & 1u;
+          uint8_t *pa = reg + 2 * (uint64_t)ti;
+          if (par && na) *reinterpret_cast<uint16_t *>(pa) = (uint16_t)tr[0];
+          u32x4a *pv = reinterpret_cast<u32x4a *>(pa + 2 * par);
+          uint32_t *pw = reinterpret_cast<uint32_t *>(pa + 2 * par);
+          // dword q: tokens par + 2q, par + 2q + 1
+          auto dw = [&](auto Q) {
+            constexpr int q = decltype(Q)::value;
+            const uint32_t nx = q + 1 < kTR / 2 ? tr[q + 1 < kTR / 2 ? q + 1 : q] : 0u;
+            return par ? __builtin_amdgcn_alignbit(nx, tr[q], 16) : tr[q];
+          };
+          sfor<0, kTR / 8>([&](auto C) {
+            constexpr int c = decltype(C)::value;
+            const uint32_t a0 = dw(std::integral_constant<int, 4 * c>{}), a1 = dw(std::integral_constant<int, 4 * c + 1>{});
+            const uint32_t a2 = dw(std::integral_constant<int, 4 * c + 2>{}), a3 = dw(std::integral_constant<int, 4 * c + 3>{});
+            if (par + 8 * c + 8 <= na) {
+              pv[c] = u32x4a{a0, a1, a2, a3};
+            } else if (par + 8 * c < na) {  // the run ends in this chunk: dwords, then a last single token
+              const uint32_t a[4] = {a0, a1, a2, a3};
+#pragma unroll
+              for (int k = 0; k < 4; k++) {
+                if (par + 8 * c + 2 * k + 2 <= na) pw[4 * c + k] = a[k];
+                else if (par + 8 * c + 2 * k + 1 == na) *reinterpret_cast<uint16_t *>(pw + 4 * c + k) = (uint16_t)a[k];
+              }
+            }
+          });
+        }
+        WMARK(26);
+        if (__ballot(mode == kModeR) != 0) {  // mode R's path starts mid-way through phase A's: check its distances
+          int od = o;
+          uint32_t pd = 0;
+          const bool chk = mode == kModeR;
+          sfor<0, kTR>([&](auto K) {
+            constexpr int k = decltype(K)::value;
+            if ((uint32_t)k >= lo && (uint32_t)k < hi) {
+              const uint32_t t = (tr[k / 2] >> (16 * (k & 1))) & 0xffffu;
+              dst[k] = (uint16_t)t;
+              derr |= chk && t > 0x7fffu && (int)(t - 0x7fffu) > od - (int)pd;
+              od += t < 256u ? 1 : t < 512u ? (int)t - 253 : 0;
+              pd = (t >> 8) == 1u ? t - 253u : pd;
+            }
+          });
+        }
+        WMARK(27);
+        if (mode != kModeF && lo + n > (uint32_t)kTR) {  // the path goes on past step kTR (no stop before it)
+          ti = ti - lo + kTR;
+          o = o0 + (int)(mode == kModeA ? bytR : rjby + bytR - rjcb);
+          run(stR, seg_end);
         }
       }
-      WMARK(5);
+      WMARK(28);
       if (__ballot(derr) != 0) { ok = false; break; }
       out += (int)tot_byt;
       ntok += (int)tot_tok;
@@ -1397,7 +1544,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
 #ifdef SBAM_WAVE_STATS
   ws_[8] = __builtin_amdgcn_s_memtime() - wt0_;
   if (lane == 0)
-    for (int i = 0; i < 16; i++) atomicAdd(&g_wave_stats[i], (unsigned long long)ws_[i]);
+    for (int i = 0; i < kWaveStats; i++) atomicAdd(&g_wave_stats[i], (unsigned long long)ws_[i]);
 #endif
   if (lane == 0) {
     if (ok) {
@@ -1426,7 +1573,6 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
 // A block's LZ77 window never leaves the chip except for the far copies; HBM sees the words once and the output
 // once.  (Round 2; the round-1 design ran one lane per block with the window in HBM and was bound by the memory
 // side: 16.5x the output bytes per launch.)
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 namespace rs {
 constexpr int kSpan = 1024;   // a chunk's words start within kSpan bytes of its base
 constexpr int kFlush = 1024;  // output bytes per group store (64 lanes x 16 B)

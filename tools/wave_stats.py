@@ -19,7 +19,7 @@ f = sbam.BamFile(s.bytes(), inflate=False)
 L = sbam.load_library()
 fn = L.sbam_debug_wave_stats
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-buf = (ctypes.c_ulonglong * 16)()
+buf = (ctypes.c_ulonglong * 32)()
 f.reset(); f.run(contig_lengths=s.contig_lengths)
 fn(buf, 1)
 f.reset(); f.run(contig_lengths=s.contig_lengths)
@@ -33,6 +33,11 @@ out.update({f"{n}_pct": round(100.0 * v[i] / tot, 1) for i, n in list(enumerate(
 out["blocks"] = int(f.n_blocks)
 out["decode_ms"] = f.kernel_ms("inflate_decode")
 out["fallbacks"] = f.inflate_fallbacks()
+tok = {n: v[i] for i, n in ((14, "lanes"), (15, "lanes_phaseB"), (16, "lanes_gt64"), (17, "lanes_gt96"),
+                              (18, "lanes_gt128"), (19, "rounds_any_phaseB"), (20, "rounds_any_gt96"),
+                              (21, "rounds_any_gt64"), (22, "rounds_with_stop"), (23, "rounds_any_modeF"))}
+out["tokens"] = tok
+out["phaseC_cycles_per_round"] = {n: round(v[i] / max(v[6], 1)) for i, n in ((24, "prefix_scan"), (25, "run1"), (26, "dumpA"), (27, "dumpR"), (28, "tail"))}
 out["b_iters_per_round"] = round(v[7] / max(v[6], 1), 3)
 out["rounds_per_block"] = round(v[6] / out["blocks"], 3)
 out["cycles_per_header"] = {n: round(v[i] / max(v[9], 1)) for i, n in ((0, "rest"), (10, "cl_setup"), (11, "chain"), (12, "stage"), (1, "build"))}
