@@ -83,6 +83,8 @@ struct sbam_ctx {
   unsigned long long *d_counts = nullptr;
   // timing
   std::map<std::string, std::pair<hipEvent_t, hipEvent_t>> ev;
+  // sbam_load's copy pieces in flight (hipEventDisableTiming events, created on first use)
+  hipEvent_t load_ev[4] = {nullptr, nullptr, nullptr, nullptr};
   sbam_error err{};
   std::string path = "<bytes>";  // Path.toString in exception messages (sbam_set_path)
 };
@@ -282,6 +284,8 @@ void sbam_close(sbam_ctx *c) {
     (void)hipEventDestroy(kv.second.first);
     (void)hipEventDestroy(kv.second.second);
   }
+  for (hipEvent_t e : c->load_ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -300,14 +304,20 @@ int sbam_load(sbam_ctx *c, const uint8_t *data, int64_t len, int64_t base_offset
   HIPCHK(c, hipStreamSynchronize(c->stream));  // the previous window's work is done with d_comp
   HIPCHK(c, ensure(&c->d_comp, &c->comp_cap, (size_t)len + kCompPad));
   HIPCHK(c, hipMemsetAsync(c->d_comp + len, 0, kCompPad, c->stream));
-  // in 8 MiB pieces, each waited for: a multi-GB copy queued whole would hold the copy engine, and the small
-  // copies of another context's kernels running meanwhile (results, tables) would wait behind it
-  // (tools/e2e_probe.py: a window's compute 56 -> 98 ms while the next window's 2.5 GB copy ran)
+  // in 8 MiB pieces with at most kInFlight queued: a multi-GB copy queued whole would hold the copy engine, and the
+  // small copies of another context's kernels running meanwhile (results, tables) would wait behind it
+  // (tools/e2e_probe.py: a window's compute 56 -> 98 ms while the next window's 2.5 GB copy ran); a few pieces in
+  // flight keep the engine busy without a host round trip between pieces
   constexpr int64_t kPiece = 8ll << 20;
-  for (int64_t o = 0; o < len; o += kPiece) {
+  constexpr int kInFlight = 3;
+  for (hipEvent_t &e : c->load_ev)
+    if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  int64_t k = 0;
+  for (int64_t o = 0; o < len; o += kPiece, k++) {
+    if (k >= kInFlight) HIPCHK(c, hipEventSynchronize(c->load_ev[(k - kInFlight) % 4]));
     const int64_t n = std::min(kPiece, len - o);
     HIPCHK(c, hipMemcpyAsync(c->d_comp + o, data + o, (size_t)n, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipEventRecord(c->load_ev[k % 4], c->stream));
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   // another file (or a range from its start): its contig lengths must come from sbam_header /

@@ -741,7 +741,10 @@ constexpr int kCpSteps = 8;        // symbols between checkpoints
 // the left neighbour's exit and phase A's counts from the entry on need no phase-B re-decode.  Decode at 10 GB:
 // no warm-up 79.5 ms; 128 bits 74.8; 256: 71.6; 384: 69.6; 512 (one segment; lane 1 from the round's true start):
 // 68.5; 640: 70.1; 1024: 76.7.
-constexpr int kWarm = kK;
+#ifndef SBAM_WARM
+#define SBAM_WARM kK
+#endif
+constexpr int kWarm = SBAM_WARM;
 // Phase A keeps the tokens of its first kTR symbol steps in registers (two per VGPR, step j in half j & 1 of
 // tr[j / 2]: the steps are unrolled, so every index is static).  A lane whose phase-A path is the true one (the
 // common case after the warm-up) then only stores them in phase C; it decodes again only past step kTR.

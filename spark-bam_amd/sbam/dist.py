@@ -473,34 +473,40 @@ class WindowPipe:
     """A rank's byte range streamed through two contexts in W windows (`wplans`: the windows' ShardPlans): while
     window w computes on one context, a loader thread copies window w+1's bytes into the other (sbam_load's host →
     device copy) and a stager thread stages window w+2 into host memory (`stage(lo, hi, k)` into staging buffer
-    k = w mod 3).  A step starts with window 0 loaded in the foreground, so every step is a complete host →
-    results pass.  `run_window(shard)` is the per-window work (GpuShard.step / load_step / anything on shard.f).
-    Buffer k is restaged only after the copy that read it has finished (window w+2 reuses window w-1's buffer,
-    whose copy ended before window w-1 computed)."""
+    k).  Windows are numbered across steps (g = step · W + w): window g uses context g mod 2 and staging buffer
+    g mod 3, so the pipeline runs on from one step into the next — the last window of a step computes while the
+    next step's window 0 is copied (`prefetch=True`; `drop_prefetch()` discards one that no step will use).
+    Without a pending prefetch a step starts with window 0 loaded in the foreground.  `run_window(shard)` is the
+    per-window work (GpuShard.step / load_step / anything on shard.f).  Buffer k is restaged only after the copy
+    that read it has finished (window g+2 reuses window g-1's buffer, whose copy ended before window g-1 computed)."""
     NBUF = 3
 
-    def __init__(self, wplans, stage, split_size, contig_lengths, device, run_window, halo: int = 2 << 20):
+    def __init__(self, wplans, stage, split_size, contig_lengths, device, run_window, halo: int = 2 << 20,
+                 prefetch: bool = False):
         from concurrent.futures import ThreadPoolExecutor
         self.wplans, self.stage, self.split_size = wplans, stage, split_size
         self.contig_lengths, self.device, self.run_window, self.halo = contig_lengths, device, run_window, halo
+        self.prefetch = prefetch
         self.loader = ThreadPoolExecutor(max_workers=1)
         self.stager = ThreadPoolExecutor(max_workers=1)
         self.ctx = [None, None]
+        self.g = 0            # global number of the next step's window 0
+        self._next = None     # (load future of window g, {g': staged future}) carried over from the last step
 
-    def _range(self, w):
-        sh = self.ctx[w % 2]
-        return self.wplans[w].load_range(sh.halo if sh is not None else self.halo)
+    def _range(self, g):
+        sh = self.ctx[g % 2]
+        return self.wplans[g % len(self.wplans)].load_range(sh.halo if sh is not None else self.halo)
 
-    def _stage(self, w):
-        lo, hi = self._range(w)
-        return lo, hi, self.stage(lo, hi, w % self.NBUF)
+    def _stage(self, g):
+        lo, hi = self._range(g)
+        return lo, hi, self.stage(lo, hi, g % self.NBUF)
 
-    def _load(self, w, staged):
-        wp = self.wplans[w]
-        j, k = w % 2, w % self.NBUF
+    def _load(self, g, staged):
+        wp = self.wplans[g % len(self.wplans)]
+        j, k = g % 2, g % self.NBUF
         lo, hi, buf = staged.result()
-        if (lo, hi) != self._range(w):  # the context's halo grew since staging: stage again
-            lo, hi = self._range(w)
+        if (lo, hi) != self._range(g):  # the context's halo grew since staging: stage again
+            lo, hi = self._range(g)
             buf = self.stage(lo, hi, k)
         src = self._source(lo, hi, buf)
         if self.ctx[j] is None:
@@ -516,20 +522,42 @@ class WindowPipe:
             return buf if (a, b) == (lo, hi) else self.stage(a, b, None)
         return src
 
+    def drop_prefetch(self):
+        """Wait for and discard a prefetched window 0 (the next step then loads it in the foreground)."""
+        if self._next is not None:
+            fut, staged = self._next
+            fut.result()
+            for f in staged.values():
+                f.result()
+            self._next = None  # window self.g is loaded again (same context) by the next step
+
     def step(self) -> list:
         W = len(self.wplans)
+        g0 = self.g
         out = []
-        staged = {w: self.stager.submit(self._stage, w) for w in range(min(2, W))}
-        sh = self._load(0, staged[0])
-        fut = None
+        if self._next is not None:
+            fut, staged = self._next
+            self._next = None
+        else:
+            staged = {g: self.stager.submit(self._stage, g) for g in range(g0, g0 + min(2, W))}
+            fut = None
+        sh = self._load(g0, staged[g0]) if fut is None else None
         for w in range(W):
-            if w > 0:
+            g = g0 + w
+            if sh is None:
                 sh = fut.result()
-            if w + 1 < W:
-                fut = self.loader.submit(self._load, w + 1, staged[w + 1])
-            if w + 2 < W:
-                staged[w + 2] = self.stager.submit(self._stage, w + 2)
+            last = w + 1 == W
+            if not last or self.prefetch:
+                if g + 1 not in staged:
+                    staged[g + 1] = self.stager.submit(self._stage, g + 1)
+                fut = self.loader.submit(self._load, g + 1, staged[g + 1])
+            if (w + 2 < W or self.prefetch) and g + 2 not in staged:
+                staged[g + 2] = self.stager.submit(self._stage, g + 2)
             out.append(self.run_window(sh))
+            sh = None
+        self.g = g0 + W
+        if self.prefetch:
+            self._next = (fut, {k: v for k, v in staged.items() if k >= self.g})
         return out
 
     def close(self):

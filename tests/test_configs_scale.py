@@ -74,7 +74,8 @@ def test_configs2_eight_shards_exact(tmp_path, distinct_synth):
 
 
 @pytest.mark.gpu
-def test_configs3_streamed_windows_equal_resident():
+@pytest.mark.parametrize("prefetch", [False, True])
+def test_configs3_streamed_windows_equal_resident(prefetch):
     import oracle
     import sbam
     import synth
@@ -91,10 +92,12 @@ def test_configs3_streamed_windows_equal_resident():
         st = sh.f.blocks()[0]
         return sizes, c, int(st[0]) if st.size else s.size
 
-    pipe = sdist.WindowPipe(wplans, lambda lo, hi, j: s.slice(lo, hi), SPLIT, s.contig_lengths, 0, run_window)
+    pipe = sdist.WindowPipe(wplans, lambda lo, hi, j: s.slice(lo, hi), SPLIT, s.contig_lengths, 0, run_window,
+                            prefetch=prefetch)
     try:
-        for _ in range(2):  # the second step reuses both contexts (sbam_load)
+        for _ in range(3):  # later steps reuse both contexts (sbam_load); with prefetch, window 0 loads early
             got = pipe.step()
+        pipe.drop_prefetch()
     finally:
         pipe.close()
     with sbam.BamFile(data, path="synth.bam") as f:

@@ -146,8 +146,9 @@ class TestLongReadsGpu:
         assert u["n_success"] == ns == s.n_records
         assert grew >= 1, "no shard needed a larger halo: the test does not reach the halo path"
 
-    @pytest.mark.parametrize("windows,split_size", [(4, 256 * 1024), (6, 64 * 1024)])
-    def test_window_pipe_halo_growth_reused_buffers(self, long_file, windows, split_size):
+    @pytest.mark.parametrize("windows,split_size,prefetch", [(4, 256 * 1024, False), (6, 64 * 1024, False),
+                                                          (3, 256 * 1024, True)])
+    def test_window_pipe_halo_growth_reused_buffers(self, long_file, windows, split_size, prefetch):
         """sbam.dist.WindowPipe (bench --windows) with a 64 KiB halo over long reads: contexts grow their halo and
         re-read their range inside the pipe while the stager and loader threads reuse three staging buffers.  A halo
         retry must read private bytes (stage(lo, hi, None)), never a shared slot: the combined result equals the
@@ -167,11 +168,11 @@ class TestLongReadsGpu:
 
         wplans = sdist.plan_shards(s.size, split_size, windows)
         pipe = sdist.WindowPipe(wplans, stage, split_size, s.contig_lengths, 0, lambda sh: sh.step(),
-                                halo=64 * 1024)
+                                halo=64 * 1024, prefetch=prefetch)
         want, parts = oracle.compute_splits(o, split_size)
         c, npos, rbe, ns = o.counts_parallel(0, o.L, 10, 8)
         try:
-            for _ in range(2):
+            for _ in range(3 if prefetch else 2):  # (an odd window count with prefetch alternates the contexts)
                 results = pipe.step()
                 counts = np.sum([r.counts for r in results], axis=0)
                 results = [sdist.ShardResult(counts if i == 0 else np.zeros_like(counts), r.first_block_pos,
