@@ -37,6 +37,8 @@ struct sbam_ctx {
   int32_t *d_cc = nullptr;
   int64_t *d_coff = nullptr;
   size_t cc_cap = 0, coff_cap = 0;
+  Candidate *d_slots = nullptr;  // one-pass scan: kScanSlots per chunk
+  size_t slots_cap = 0;
   // block table (relative offsets), device + host
   int64_t nblocks = -1;
   int64_t *d_bstart = nullptr, *d_buoff = nullptr;
@@ -259,6 +261,7 @@ void sbam_close(sbam_ctx *c) {
   dfree(c->d_cand);
   dfree(c->d_cc);
   dfree(c->d_coff);
+  dfree(c->d_slots);
   dfree(c->d_status);
   dfree(c->d_found);
   dfree(c->d_bstart);
@@ -357,13 +360,20 @@ static int scan_candidates(sbam_ctx *c) {
   const int64_t nchunks = (c->D + kScanChunk - 1) / kScanChunk;
   HIPCHK(c, ensure(&c->d_cc, &c->cc_cap, nchunks));
   HIPCHK(c, ensure(&c->d_coff, &c->coff_cap, nchunks));
-  HIPCHK(c, launch_scan_count(c->d_comp, c->D, c->d_cc, nchunks, c->stream));
+  HIPCHK(c, ensure(&c->d_slots, &c->slots_cap, (size_t)nchunks * kScanSlots));
+  // one pass into per-chunk slots (+ counts, exact even past the slots); d_small[0] = total, [1] = overflow
+  HIPCHK(c, launch_scan_slots(c->d_comp, c->D, c->d_cc, nchunks, c->d_slots, c->d_small + 1, c->stream));
   HIPCHK(c, launch_scan_prefix(c->d_cc, nchunks, c->d_coff, c->d_small, c->stream));
-  int64_t total = 0;
-  HIPCHK(c, hipMemcpyAsync(&total, c->d_small, sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  int64_t tot_ovf[2] = {0, 0};
+  HIPCHK(c, hipMemcpyAsync(tot_ovf, c->d_small, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  const int64_t total = tot_ovf[0];
   HIPCHK(c, ensure(&c->d_cand, &c->cand_cap, total));
-  HIPCHK(c, launch_scan_write(c->d_comp, c->D, c->d_coff, nchunks, c->d_cand, c->stream));
+  if (tot_ovf[1] == 0) {
+    HIPCHK(c, launch_scan_compact(c->d_slots, c->d_cc, c->d_coff, nchunks, c->d_cand, c->stream));
+  } else {  // a chunk with more than kScanSlots candidates (blocks under 2 KiB): the exact second pass
+    HIPCHK(c, launch_scan_write(c->d_comp, c->D, c->d_coff, nchunks, c->d_cand, c->stream));
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->ncand = total;
   return SBAM_OK;

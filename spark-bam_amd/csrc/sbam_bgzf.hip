@@ -163,6 +163,70 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_write(const uint8_t *__re
   }
 }
 
+// One-pass form (round 3): the same candidates written to chunk b's kScanSlots fixed slots, its count to
+// chunk_counts[b] (slots past kScanSlots are not written; *overflow is set and the caller runs k_scan_write with
+// the exact offsets instead), then k_scan_compact moves the slots into file order.  Reads the compressed bytes
+// once instead of twice (k_scan_count + k_scan_write).
+__global__ __launch_bounds__(kScanThreads) void k_scan_slots(const uint8_t *__restrict__ d, int64_t D,
+                                                              int32_t *__restrict__ chunk_counts,
+                                                              Candidate *__restrict__ slots,
+                                                              unsigned long long *__restrict__ overflow) {
+  const int64_t cbase = (int64_t)blockIdx.x * kScanChunk;
+  const int64_t cend = min(cbase + (int64_t)kScanChunk, D);
+  __shared__ int s_any;
+  __shared__ int s_wsum[kScanThreads / 64];
+  Candidate *out = slots + (int64_t)blockIdx.x * kScanSlots;
+  int run = 0;
+  for (int64_t it = cbase; it < cend; it += kScanStep) {
+    const int64_t q0 = it + threadIdx.x * 16;
+    uint32_t bits = 0;
+    if (q0 < cend) {
+      uint32_t w[8];
+      load32(d, q0, w);
+      bits = header_bits16(w, q0, D);
+      if (q0 + 16 > cend) bits &= (1u << (cend - q0)) - 1u;
+    }
+    if (threadIdx.x == 0) s_any = 0;
+    __syncthreads();
+    if (bits) s_any = 1;
+    __syncthreads();
+    if (s_any) {  // rare: ordered rank = wave prefix + preceding waves
+      const int c = __popc(bits);
+      int incl = c;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (lane_id() >= o) incl += t;
+      }
+      if (lane_id() == 63) s_wsum[threadIdx.x >> 6] = incl;
+      __syncthreads();
+      int before = incl - c;
+      for (int wv = 0; wv < (int)(threadIdx.x >> 6); wv++) before += s_wsum[wv];
+      int slot = run + before;
+      while (bits) {
+        const int i = __ffs(bits) - 1;
+        bits &= bits - 1;
+        if (slot < kScanSlots) fill_candidate(d, D, q0 + i, out[slot]);
+        slot++;
+      }
+      run += s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    chunk_counts[blockIdx.x] = run;
+    if (run > kScanSlots) atomicOr(overflow, 1ull);
+  }
+}
+
+// slots -> file order: slot j of chunk b goes to chunk_off[b] + j (j < chunk_counts[b] <= kScanSlots)
+__global__ void k_scan_compact(const Candidate *__restrict__ slots, const int32_t *__restrict__ cnt,
+                               const int64_t *__restrict__ off, int64_t nchunks, Candidate *__restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t b = i / kScanSlots;
+  const int j = (int)(i % kScanSlots);
+  if (b < nchunks && j < cnt[b]) out[off[b] + j] = slots[i];
+}
+
 // MetadataStream chain test: per candidate i (>= first), code 0 = the next header sits at cands[i+1];
 // 1 = stop before emitting i (ISIZE past EOF, or empty block); 2 = emit i then EOF inside the next header;
 // 3 = next header not at cands[i+1] (false positive in between, or corruption: host walks exactly).
@@ -253,6 +317,22 @@ hipError_t launch_scan_write(const uint8_t *d, int64_t D, const int64_t *off, in
                              hipStream_t s) {
   if (nchunks == 0) return hipSuccess;
   hipLaunchKernelGGL(k_scan_write, dim3((unsigned)nchunks), dim3(kScanThreads), 0, s, d, D, off, c);
+  return hipGetLastError();
+}
+hipError_t launch_scan_slots(const uint8_t *d, int64_t D, int32_t *cc, int64_t nchunks, Candidate *slots,
+                             int64_t *overflow, hipStream_t s) {
+  (void)hipMemsetAsync(overflow, 0, sizeof(int64_t), s);
+  if (nchunks == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scan_slots, dim3((unsigned)nchunks), dim3(kScanThreads), 0, s, d, D, cc, slots,
+                     reinterpret_cast<unsigned long long *>(overflow));
+  return hipGetLastError();
+}
+hipError_t launch_scan_compact(const Candidate *slots, const int32_t *cc, const int64_t *off, int64_t nchunks,
+                               Candidate *out, hipStream_t s) {
+  const int64_t n = nchunks * kScanSlots;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scan_compact, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, slots, cc, off, nchunks,
+                     out);
   return hipGetLastError();
 }
 hipError_t launch_chain_verify(const Candidate *c, int64_t n, int64_t first, int64_t D, int64_t *first_stop,

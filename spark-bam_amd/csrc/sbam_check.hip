@@ -1032,10 +1032,9 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
 //     transposed across 8 lanes (ds_swizzle) into bitmap dwords.
 // A position with a long name or op array (past the 64 bytes / ops one bitmap read covers) is redone by check_first
 // and patched into the planes.  Interior tiles only (no EOF in reach), R > 0, n_ref <= kLdsLens (lengths in LDS).
-SB_DEV uint32_t push_bit(uint32_t p, bool c) {
-  uint32_t r;
-  uint64_t co;
-  asm("v_addc_co_u32 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(p), "s"(__ballot(c)));
+SB_DEV uint32_t push_bit(uint32_t p, bool c) {  // (the carry-out goes to VCC: a dead SGPR-pair output made the
+  uint32_t r;                                    // compiler reuse one pair and pad with s_nop between VALU writes)
+  asm("v_addc_co_u32 %0, vcc, %1, %1, %2" : "=v"(r) : "v"(p), "s"(__ballot(c)) : "vcc");
   return r;
 }
 // One stage of an 8 x 8 transpose of nibbles across 8 lanes (nibble j of lane li -> nibble li of lane j): exchange
@@ -1066,7 +1065,9 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bi
   __shared__ uint32_t s_opc[4 * kOpcWords];
   __shared__ uint32_t s_nbad[kNameWords];
   __shared__ __attribute__((aligned(16))) uint8_t s_fb[kFbBytes];  // first invalid op from each byte (stage_fb)
-  __shared__ uint32_t s_pl[3][kCheckThreads + 8];  // per lane: I < -1, I >= n_ref, 0 <= I < n_ref && I(+4) > len[I]
+  // per lane and byte offset y of its 32: I(y) < -1, I(y) >= n_ref, 0 <= I(y) < n_ref && I(y + 4) > len[I(y)],
+  // byte(y) == 0, byte(y) == 1, byte(y) > 64 (I(y): the int32 at y)
+  __shared__ uint32_t s_pl[6][kCheckThreads + 8];
   __shared__ unsigned long long s_acc[19 + 21];     // totals, positions per key
   __shared__ uint32_t s_k12[3 * 19];
   __shared__ uint32_t s_pair[19 * 19];
@@ -1104,37 +1105,59 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bi
     __syncthreads();
     stage_fb(s_win, s_opc, s_fb);
     // ---- predicate pass over the offsets 1024 j + 4 t + o; lanes t < 8 add row 8 (offsets 8192 + 4 t + o), which
-    // shifts row 0 out and leaves exactly the planes of lanes 256 + t
+    // shifts row 0 out and leaves exactly the planes of lanes 256 + t.  The contig-length test reads the length table
+    // only at offsets whose int32 is a contig index (a bit loop over that plane: ~1 % of offsets)
     {
-      uint32_t pa = 0, pb = 0, pc = 0;
+      uint32_t pa = 0, pb = 0, pin = 0, pz = 0, pe = 0, pg = 0;
       auto row = [&](int j) {
         const int g = j * kCheckThreads + t;
-        const uint32_t W0 = w32[g], W1 = w32[g + 1], W2 = w32[g + 2];
+        const uint32_t W0 = w32[g], W1 = w32[g + 1];
 #pragma unroll
         for (int o = 0; o < 4; o++) {
           const int32_t I = (int32_t)(o == 0 ? W0 : __builtin_amdgcn_alignbyte(W1, W0, o));
-          const int32_t I4 = (int32_t)(o == 0 ? W1 : __builtin_amdgcn_alignbyte(W2, W1, o));
-          const int32_t len = s_lens[min((uint32_t)I, (uint32_t)nref)];  // INT_MAX unless 0 <= I < n_ref
+          const uint32_t by = (uint32_t)I & 0xffu;
           pa = push_bit(pa, I < -1);
           pb = push_bit(pb, I >= nref);
-          pc = push_bit(pc, I4 > len);
+          pin = push_bit(pin, (uint32_t)I < (uint32_t)nref);
+          pz = push_bit(pz, by == 0);
+          pe = push_bit(pe, by == 1);
+          pg = push_bit(pg, by > 64);
         }
+      };
+      // I(y + 4) > len[I(y)] where I(y) is a contig index; r0: the row of plane bit 31 (1 for lanes 256 + t)
+      auto bigpos = [&](uint32_t in, int r0) {
+        uint32_t pc = 0;
+        for (uint32_t q = in; q; q &= q - 1u) {
+          const int b = __builtin_ctz(q), k = 31 - b;
+          const int y = 4 * (((k >> 2) + r0) * kCheckThreads + t) + (k & 3);
+          const int32_t I = (int32_t)__builtin_amdgcn_alignbyte(w32[(y >> 2) + 1], w32[y >> 2], y & 3);
+          const int32_t I4 = (int32_t)__builtin_amdgcn_alignbyte(w32[(y >> 2) + 2], w32[(y >> 2) + 1], y & 3);
+          pc |= I4 > s_lens[I] ? (1u << b) : 0u;
+        }
+        return pc;
       };
 #pragma unroll 1
       for (int j = 0; j < 8; j++) row(j);
       s_pl[0][t] = pa;
       s_pl[1][t] = pb;
-      s_pl[2][t] = pc;
+      s_pl[2][t] = bigpos(pin, 0);
+      s_pl[3][t] = pz;
+      s_pl[4][t] = pe;
+      s_pl[5][t] = pg;
       if (t < 8) {
         row(8);
         s_pl[0][kCheckThreads + t] = pa;
         s_pl[1][kCheckThreads + t] = pb;
-        s_pl[2][kCheckThreads + t] = pc;
+        s_pl[2][kCheckThreads + t] = bigpos(pin, 1);
+        s_pl[3][kCheckThreads + t] = pz;
+        s_pl[4][kCheckThreads + t] = pe;
+        s_pl[5][kCheckThreads + t] = pg;
       }
     }
     __syncthreads();
-    // ---- per-record predicates
-    uint32_t pLZ = 0, pIV = 0, pTF = 0, pNG = 0, pZ = 0, pO = 0, pFL = 0, pLS = 0, pNC = 0;
+    // ---- per-record predicates; the byte-local ones come from the byte planes of the lanes 3-5 to the right
+    // (a field at byte offset 4q + K of position x is byte plane bit x + 4q + K: lane t + q, shifted by K)
+    uint32_t pLZ = 0, pIV = 0, pTF = 0, pFL = 0;
 #pragma unroll 1
     for (int j = 0; j < 8; j++) {
       const int g = j * kCheckThreads + t;
@@ -1152,17 +1175,31 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bi
         const int32_t nc = (int32_t)(fld(4) & 0xffffu);
         const int32_t ls = (int32_t)fld(5);
         const uint32_t last = s_win[rel + 35 + lrn];  // the name's last byte (read for lrn < 2 too, unused then)
-        // first invalid op (>= 64: none among the first 64)
-        const uint32_t obad = s_fb[rel + 36 + (lrn >= 2 ? lrn : 0)];
+        // first invalid op (>= 64: none among the first 64); ops start at 36 + lrn, or 36 when lrn < 2: lrn = 0
+        // reads the right byte, lrn = 1 is redone below
+        const uint32_t obad = s_fb[rel + 36 + lrn];
         pLZ = push_bit(pLZ, last == 0);
         pIV = push_bit(pIV, obad < min((uint32_t)nc, 64u));  // an invalid op among the first min(nc, 64)
         pTF = push_bit(pTF, too_few_remaining(bs, lrn, nc, ls));
-        pNG = push_bit(pNG, nc > 64);  // op array past the 64 checked ops
-        pZ = push_bit(pZ, lrn == 0);
-        pO = push_bit(pO, lrn == 1);
-        pLS = push_bit(pLS, ls == 0);
-        pNC = push_bit(pNC, nc == 0);
       }
+    }
+    // byte planes: K = 1..3 shifts a plane by K positions (bits of a nibble move up; the top K come from lane u + 1)
+    auto shk = [&](int K, const uint32_t *P, int u) {
+      const uint32_t M = K == 1 ? 0xeeeeeeeeu : K == 2 ? 0xccccccccu : 0x88888888u;
+      return ((P[u] << K) & M) | ((P[u + 1] >> (4 - K)) & ~M);
+    };
+    const uint32_t *PZ = s_pl[3], *PE = s_pl[4], *PG = s_pl[5];
+    const uint32_t pZ = PZ[t + 3];                                                       // l_read_name == 0
+    const uint32_t pO = PE[t + 3];                                                       // l_read_name == 1
+    const uint32_t z17 = shk(1, PZ, t + 4);
+    const uint32_t pNC = PZ[t + 4] & z17;                                                 // n_cigar == 0
+    const uint32_t pNG = ~z17 | PG[t + 4];                                                // n_cigar > 64
+    const uint32_t pLS = PZ[t + 5] & shk(1, PZ, t + 5) & shk(2, PZ, t + 5) & shk(3, PZ, t + 5);  // l_seq == 0
+    // l_read_name == 1: the ops start at 36, not 37
+    for (uint32_t q = pO; q; q &= q - 1u) {
+      const int b = __builtin_ctz(q), k = 31 - b, rel = 4 * ((k >> 2) * kCheckThreads + t) + (k & 3);
+      const uint32_t nc = (uint32_t)s_win[rel + 16] | ((uint32_t)s_win[rel + 17] << 8);
+      pIV = (pIV & ~(1u << b)) | (s_fb[rel + 36] < min(nc, 64u) ? (1u << b) : 0u);
     }
     // the name characters matter only where the name ends in NUL (true records and ~1/256 of the rest): those
     // positions are checked one by one, and so are the op arrays longer than 64 ops whose first 64 are valid
@@ -1267,7 +1304,7 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bi
 // first tested on those two fields alone (two funnel shifts and two compares per position); only the survivors —
 // true record starts and the few positions whose indices happen to be small — are queued per wave and checked in
 // full (eager_pass_direct, all 64 lanes on queued positions).  Same PASS0 bitmap as k_check<MODE_EAGER, 1>.
-constexpr int kEagerQ = 512;       // per-wave queue of survivors (a tile's are queued in rounds of this many)
+constexpr int kEagerQ = 2048;      // workgroup queue of survivors (a tile's are queued in rounds of this many)
 constexpr int kEagerLens = 1024;   // contig lengths in LDS (more: read from HBM) — keeps 8 workgroups per CU
 // eager.Checker at an interior position whose indices passed the prefilter, straight from the staged bytes (no
 // op-class / name-character bitmaps: survivors are few, and a true record's name and CIGAR are short).  Same
@@ -1283,9 +1320,14 @@ SB_DEV bool eager_pass_direct(const uint8_t *win, const StreamView &sv, const in
   if (rb0 | rb1 | (too_few_remaining(bs, lrn, nc, ls) ? 1u : 0u)) return false;
   if (lrn < 2 || ((flag & 4u) == 0 && (ls == 0 || nc == 0))) return false;
   if (win[rel + 35 + lrn] != 0) return false;  // name not NUL-terminated
-  for (int i = 0; i < lrn - 1; i++) {
-    const uint32_t c = win[rel + 36 + i];
-    if (!((c - 33u <= 30u) || (c - 65u <= 61u))) return false;  // allowedReadNameChars
+  // allowedReadNameChars, 4 name bytes per step (SWAR over an unaligned dword of the window)
+  const uint32_t *w32 = reinterpret_cast<const uint32_t *>(win);
+  for (int i = 0; i < lrn - 1; i += 4) {
+    const int a = rel + 36 + i;
+    const uint32_t w = __builtin_amdgcn_alignbyte(w32[(a >> 2) + 1], w32[a >> 2], (uint32_t)a & 3u);
+    const int left = lrn - 1 - i;
+    const uint32_t keep = left >= 4 ? 0x80808080u : (0x80808080u >> (8 * (4 - left)));
+    if (name_bad_bytes(w) & keep) return false;
   }
   const int c0 = rel + 36 + lrn;
   const int in_win = min(nc, (kWin - c0) >> 2);  // ops inside the staged window, then HBM
@@ -1302,7 +1344,8 @@ __global__ __launch_bounds__(kCheckThreads) void k_eager(StreamView sv, int64_t 
                                                          int64_t thi) {
   __shared__ __attribute__((aligned(16))) uint8_t s_win[kWin + 64];
   __shared__ int32_t s_lens[kEagerLens];
-  __shared__ uint16_t s_q[kCheckThreads / 64][kEagerQ];
+  __shared__ uint16_t s_q[kEagerQ];
+  __shared__ uint32_t s_wn[kCheckThreads / 64];  // survivors per wave
   __shared__ unsigned long long s_bits[kTile / 64];
   const int lane = lane_id(), wv = (int)threadIdx.x >> 6;
   const int32_t *lensL = nullptr;
@@ -1313,7 +1356,7 @@ __global__ __launch_bounds__(kCheckThreads) void k_eager(StreamView sv, int64_t 
   const uint32_t nref1 = (uint32_t)sv.nref;  // idx + 1 <= n_ref  <=>  -1 <= idx < n_ref
   const int64_t x0a = x0 & ~(int64_t)63;
   const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
-  uint16_t *q = s_q[wv];
+  uint16_t *q = s_q;
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   typedef const __attribute__((address_space(1))) u32x4 *g16;
   // the window of the next tile is loaded into registers while this one is checked
@@ -1365,22 +1408,32 @@ __global__ __launch_bounds__(kCheckThreads) void k_eager(StreamView sv, int64_t 
         sm = push_bit(sm, ri + 1u <= nref1 && nri + 1u <= nref1);  // position (j, o) at bit 31 - (4 j + o)
       }
     }
-    // queue the wave's survivors (kEagerQ at a time) and check them 64 at a time
+    // the workgroup's survivors go to one queue (kEagerQ at a time), drained 64 at a time by the waves in turn: a
+    // tile has ~40 (0.5 % of positions), so one wave usually checks them all in one full-width round instead of
+    // every wave running a mostly idle one
     const uint32_t n = (uint32_t)__popc(sm);
     const uint32_t incl = wave_incl_scan_u32(n);
-    const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+    if (lane == 63) s_wn[wv] = incl;
+    __syncthreads();
+    uint32_t wbase = 0, total = 0;
+#pragma unroll
+    for (int k = 0; k < kCheckThreads / 64; k++) {
+      const uint32_t c = s_wn[k];
+      wbase += k < wv ? c : 0u;
+      total += c;
+    }
     for (uint32_t r0 = 0; r0 < total; r0 += kEagerQ) {
-      uint32_t at = incl - n;
+      uint32_t at = wbase + incl - n;
       for (uint32_t m = sm; m && at < r0 + kEagerQ; m &= m - 1, at++) {
         if (at >= r0) {
           const int bit = 31 - __builtin_ctz(m);
           q[at - r0] = (uint16_t)(4 * ((bit >> 2) * kCheckThreads + (int)threadIdx.x) + (bit & 3));
         }
       }
-      __builtin_amdgcn_wave_barrier();
+      __syncthreads();
       const int nq = (int)min((uint32_t)kEagerQ, total - r0);
-      for (int from = 0; from < nq; from += 64) drain(from, min(64, nq - from));
-      __builtin_amdgcn_wave_barrier();
+      for (int from = 64 * wv; from < nq; from += kCheckThreads) drain(from, min(64, nq - from));
+      __syncthreads();
     }
     __syncthreads();
     if (threadIdx.x < kTile / 64) bitmap[((base - x0a) >> 6) + threadIdx.x] = s_bits[threadIdx.x];

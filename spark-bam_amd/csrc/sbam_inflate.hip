@@ -740,9 +740,10 @@ constexpr int kCpSteps = 8;        // symbols between checkpoints
 // resynchronised with the true one: the first symbol boundary at or after the segment start ("entry") then equals
 // the left neighbour's exit and phase A's counts from the entry on need no phase-B re-decode.  Decode at 10 GB:
 // no warm-up 79.5 ms; 128 bits 74.8; 256: 71.6; 384: 69.6; 512 (one segment; lane 1 from the round's true start):
-// 68.5; 640: 70.1; 1024: 76.7.
+// 68.5; 640: 70.1; 1024: 76.7.  Round 3 (544-bit segments, register tokens, re-decode only to the rejoin point):
+// 192: 70.5; 288: 65.7; 384: 59.9; 544: 51.1; 640: 49.6; 768: 49.8; 960: 52.2.
 #ifndef SBAM_WARM
-#define SBAM_WARM kK
+#define SBAM_WARM 640
 #endif
 constexpr int kWarm = SBAM_WARM;
 // Phase A keeps the tokens of its first kTR symbol steps in registers (two per VGPR, step j in half j & 1 of
@@ -811,14 +812,17 @@ struct CanonW {
   uint32_t lim[16];
   int32_t base[16];
 };
-SB_DEV uint32_t canon_len(const CanonW &c, uint32_t v) {  // code length of the 15-bit left-justified code v
+// code length of the 15-bit left-justified code v, known to be at most MAXL (root entries: the root bits)
+template <int MAXL = 15>
+SB_DEV uint32_t canon_len(const CanonW &c, uint32_t v) {
   uint32_t l = 1;
-  sfor<1, 15>([&](auto I) { l += v >= c.lim[decltype(I)::value] ? 1u : 0u; });
+  sfor<1, MAXL>([&](auto I) { l += v >= c.lim[decltype(I)::value] ? 1u : 0u; });
   return l;
 }
+template <int MAXL = 15>
 SB_DEV int32_t canon_base(const CanonW &c, uint32_t l) {  // c.base[l] by selects (a runtime index would
   int32_t r = 0;                                            // move the whole struct to scratch memory)
-  sfor<1, 16>([&](auto I) { r = l == (uint32_t)decltype(I)::value ? c.base[decltype(I)::value] : r; });
+  sfor<1, MAXL + 1>([&](auto I) { r = l == (uint32_t)decltype(I)::value ? c.base[decltype(I)::value] : r; });
   return r;
 }
 
@@ -894,9 +898,9 @@ SB_DEV bool wave_build(WaveLds &L, int off, int nsym, int toff, int subcap) {
   // root entries: stream bits e (LSB first) = code prefix bitrev(e) (MSB first)
   for (int e = lane; e < (1 << R); e += 64) {
     const uint32_t v = (__builtin_bitreverse32((uint32_t)e) >> (32 - R)) << (15 - R);
-    if (v < c.lim[R]) {
-      const uint32_t l = canon_len(c, v);
-      tab[root_slot<R>((uint32_t)e)] = sym_entry(sorted[off + (int)(v >> (15 - l)) + canon_base(c, l)], l, DIST);
+    if (v < c.lim[R]) {  // a code of at most R bits
+      const uint32_t l = canon_len<R>(c, v);
+      tab[root_slot<R>((uint32_t)e)] = sym_entry(sorted[off + (int)(v >> (15 - l)) + canon_base<R>(c, l)], l, DIST);
     }
   }
   // sub-tables: one per root prefix of the codes longer than R, sized by the longest code under that prefix
@@ -1565,8 +1569,8 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
 // takes the next 64 words, one per lane:
 //   1. a wave prefix sum of the words' output lengths gives every word its position O (a chunk is cut where a word
 //      would start kSpan or more bytes after the chunk's base, and at the block's end);
-//   2. the ring dwords the chunk will write are zeroed, then every byte is written by an LDS OR of its (masked,
-//      shifted) dword — lanes writing neighbouring bytes of one dword never race;
+//   2. the ring dwords the chunk will write are zeroed, then literal bytes are written by byte stores and match
+//      bytes by LDS ORs of their (masked, shifted) dwords — lanes writing neighbouring bytes of one dword never race;
 //   3. literal words are written at once; matches go in rounds: a match is ready when its source ends at or before
 //      the first pending match of the chunk (the first pending one always is), ready matches copy in steps of up
 //      to 16 bytes (an overlapping copy doubles its distance per step) from the ring (distance <= kNear) or, for
@@ -1666,7 +1670,6 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
     if (E <= B) break;  // (no output left in the tokens: never for a decoded stream)
     // the next chunk starts after the last taken lane's tokens (and the distance its second token may own)
     const int tp2 = uni(tp + 2 * nt + (int)((__ballot(bLen) >> (nt - 1)) & 1ull));
-    const uint32_t ta2 = tk[tp2 + 2 * lane], tb2 = tk[tp2 + 2 * lane + 1], tn2 = tk[tp2 + 2 * lane + 2];
     // ---- 2. zero the ring dwords of [Z, E)
     {
       const uint32_t z0 = (Gr + (uint32_t)Z) >> 2, z1 = (Gr + (uint32_t)E + 3u) >> 2;
@@ -1681,14 +1684,18 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
       Z = (int)(z1 * 4u - Gr);
     }
     // ---- 3a. literals (before the match when a lane has both)
+    // (byte stores: they touch only their own byte, so lanes writing neighbouring bytes of a dword never race)
     const int Ll = take ? min(nl, ae - O) : 0;
     if (Ll > 0) {
       const uint32_t lv = aLit ? (ta | (bLit ? tb << 8 : 0u)) : tb;
-      const uint32_t v = lv & (Ll >= 2 ? 0xffffu : 0xffu);
-      const uint32_t x = (Gr + (uint32_t)O) & G::kMask, q = x >> 2, s8 = (x & 3u) * 8u;
-      const uint64_t sv = (uint64_t)v << s8;
-      ring_or1<G>(ring, q, (uint32_t)sv);
-      if ((uint32_t)(sv >> 32)) ring_or1<G>(ring, (q + 1u) & G::kDwMask, (uint32_t)(sv >> 32));
+      const uint32_t x = (Gr + (uint32_t)O) & G::kMask;
+      ring8[x] = (uint8_t)lv;
+      if (x < 4u * G::kMirror) ring8[G::kRing + x] = (uint8_t)lv;
+      if (Ll >= 2) {
+        const uint32_t x1 = (x + 1u) & G::kMask;
+        ring8[x1] = (uint8_t)(lv >> 8);
+        if (x1 < 4u * G::kMirror) ring8[G::kRing + x1] = (uint8_t)(lv >> 8);
+      }
     }
     // ---- 3b. matches, in rounds
     const int mO = O + (bLen ? nl : 0);
@@ -1703,6 +1710,8 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
       pf0 = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(ob + mO - d));
       if (Le > 16) pf1 = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(ob + mO - d + 16));
     }
+    // the next step's tokens, loaded after the far sources: a wait for a far source need not wait for them
+    const uint32_t ta2 = tk[tp2 + 2 * lane], tb2 = tk[tp2 + 2 * lane + 1], tn2 = tk[tp2 + 2 * lane + 2];
     const uint64_t farm = __ballot(mt && far);
     uint64_t pend = __ballot(mt);
     while (pend) {

@@ -53,10 +53,15 @@ struct RecordColumnsDev {
 };
 
 constexpr int kScanChunk = 1 << 20;  // bytes per workgroup in the BGZF candidate scan
+constexpr int kScanSlots = 512;      // candidate slots per chunk in the one-pass scan (>= 2 KiB per block)
 constexpr int kStreamPad = 16384;  // zero pad behind the uncompressed stream (>= checker LDS window)
 constexpr int kCompPad = 256;  // zero pad behind the compressed bytes (bit-reader / input-ring lookahead)
 
 hipError_t launch_scan_count(const uint8_t *d, int64_t D, int32_t *chunk_counts, int64_t nchunks, hipStream_t s);
+hipError_t launch_scan_slots(const uint8_t *d, int64_t D, int32_t *chunk_counts, int64_t nchunks, Candidate *slots,
+                             int64_t *overflow, hipStream_t s);
+hipError_t launch_scan_compact(const Candidate *slots, const int32_t *chunk_counts, const int64_t *chunk_offsets,
+                               int64_t nchunks, Candidate *out, hipStream_t s);
 hipError_t launch_scan_prefix(int32_t *chunk_counts, int64_t nchunks, int64_t *chunk_offsets, int64_t *total,
                               hipStream_t s);
 hipError_t launch_scan_write(const uint8_t *d, int64_t D, const int64_t *chunk_offsets, int64_t nchunks,

@@ -138,3 +138,23 @@ def test_wave_decoder_takes_every_compressed_block(seed):
         assert g.inflate_fallbacks() == stored
     finally:
         g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_blocks", [300, 1500])
+def test_scan_many_small_blocks(n_blocks):
+    """The one-pass BGZF scan keeps up to 512 candidates per 1 MiB chunk; more (blocks under 2 KiB, here ~40 B) take
+    the exact two-pass path.  Both give the oracle's block table and bytes (Header.make / MetadataStream)."""
+    import sbam
+    r = np.random.default_rng(n_blocks)
+    datas = [r.integers(0, 4, int(r.integers(1, 40)), dtype=np.uint8).tobytes() for _ in range(n_blocks)]
+    data = b"".join(bgzf_block(deflate(x), len(x)) for x in datas) + EOF_BLOCK
+    assert oracle_result(data) == ("ok", b"".join(datas))
+    assert gpu_result(data) == ("ok", b"".join(datas))
+    g = sbam.BamFile(data, inflate=False)
+    try:
+        starts = g.blocks()[0]
+        want = np.cumsum([0] + [len(bgzf_block(deflate(x), len(x))) for x in datas[:-1]])
+        assert np.array_equal(starts, want)
+    finally:
+        g.close()
