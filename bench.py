@@ -216,9 +216,13 @@ def main():
     t = time.time()
     s = synth.SynthBam.for_size(int(args.size_gb * 1e9 * world), tile_mb=args.tile_mb, seed=args.seed,
                                 threads=threads, read_len=args.read_len)
-    W = max(1, args.windows)
     plans = sdist.plan_shards(s.size, split_size, world)  # rank-level plans (what all_gather sees)
     plan = plans[rank]
+    W = args.windows
+    if W == 0:  # as many windows as the shard's size, compression ratio and free HBM need (two contexts)
+        W = sdist.auto_windows(plan.owned_hi - plan.lo, lambda lo, hi: s.slice(plan.lo + lo, plan.lo + hi),
+                               sdist.device_free_bytes(local))
+    W = max(1, W)
 
     def wplans_of(nw):
         return sdist.plan_shards(s.size, split_size, world * nw)[rank * nw:(rank + 1) * nw]

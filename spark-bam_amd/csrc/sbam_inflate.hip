@@ -728,12 +728,16 @@ namespace wd {
 #endif
 constexpr int kK = SBAM_KK;                // bits per lane segment
 constexpr int kWinDw = 64 * kK / 32 + 16;  // staged input dwords per round (start alignment + lookahead)
-// A 9-bit literal/length root (zlib's choice: ENOUGH_LENS = 852 entries with sub-tables) keeps the wave's LDS at
-// 9.4 KiB, so 16 decoder waves fit a CU (a 10-bit root: 11.4 KiB, 14 waves, decode 86 → 79 ms at 10 GB).
-constexpr int kLitRoot = 9, kDistRoot = 8;
-constexpr int kLitSub = 344, kDistSub = 192;  // >= ENOUGH - root: 852 - 512 at root 9; 400 - 256 at 8
-constexpr int kLitOff = 0, kDistOff = (1 << kLitRoot) + kLitSub;
-constexpr int kTab = kDistOff + (1 << kDistRoot) + kDistSub;
+// 9-bit roots for both alphabets (zlib's ENOUGH bounds: 852 literal/length and 592 distance entries with
+// sub-tables), interleaved: the root entry of 9-bit prefix b in state st (0: literal/length, 1: distance after a
+// length) is tab[2 b + st], so one symbol's lookup address is (bits & 511) << 3 | st << 2 with no state-dependent
+// root width or table base; the sub-tables follow at kLitSubOff / kDistSubOff.  The wave's LDS is 10.0 KiB (the
+// table-build counters live in the window's scratch tail), so 16 decoder waves still fit a CU (a 10-bit literal
+// root: 11.4 KiB, 14 waves, decode 86 → 79 ms at 10 GB in round 2).
+constexpr int kLitRoot = 9, kDistRoot = 9;
+constexpr int kLitSub = 340, kDistSub = 80;  // ENOUGH - root: 852 - 512 and 592 - 512 at root 9
+constexpr int kLitSubOff = 2 << kLitRoot, kDistSubOff = kLitSubOff + kLitSub;
+constexpr int kTab = kDistSubOff + kDistSub;
 constexpr int kCp = 12;            // checkpoints per lane
 constexpr int kCpSteps = 8;        // symbols between checkpoints
 // Lanes > 0 start decoding kWarm bits before their segment, so that by the segment start their path has usually
@@ -769,21 +773,11 @@ enum : int { ST_NONE = 0, ST_EOB = 1, ST_ERR = 2, ST_OUT = 3 };
 struct WaveLds {
   uint32_t win[wd::kWinDw];
   uint32_t tab[wd::kTab];
-  uint32_t cnt[16];
   SB_DEV uint8_t *lens() { return reinterpret_cast<uint8_t *>(win + wd::kWinDw - wd::kScratchDw); }  // [320]
   SB_DEV uint16_t *sorted() { return reinterpret_cast<uint16_t *>(win + wd::kWinDw - wd::kScratchDw + 80); }  // [320]
+  SB_DEV uint32_t *cnt() { return win + wd::kWinDw - 16; }  // [16], the scratch's last dwords
 };
 
-// Root-table slot of root index i (R root bits).  SBAM_TSWZ: XOR bits 5.. into bits 0..4, so that the 2^(R-l)
-// replicated entries of a short code no longer all share one LDS bank (bank = slot mod 32).
-template <int R>
-SB_DEV uint32_t root_slot(uint32_t i) {
-#ifdef SBAM_TSWZ
-  return i ^ ((i >> 5) & ((1u << (R - 5)) - 1u));
-#else
-  return i;
-#endif
-}
 
 SB_DEV uint32_t sym_entry(uint32_t s, uint32_t l, bool dist) {
   using namespace wd;
@@ -844,21 +838,22 @@ SB_DEV uint32_t wave_incl_scan(uint32_t x) {
   return x;
 }
 
-// Decode table of one alphabet from lens[off, off + nsym), by the whole wave, into tab[toff, ...).  Returns false
-// (wave-uniform) for a code set that is not complete (zlib rejects over-subscribed ones and most incomplete ones;
-// the slow decoder handles every such block exactly) or whose sub-tables would not fit.
+// Decode table of one alphabet from lens[off, off + nsym), by the whole wave: root entries at tab[2 b + DIST],
+// sub-tables from tab[suboff].  Returns false (wave-uniform) for a code set that is not complete (zlib rejects
+// over-subscribed ones and most incomplete ones; the slow decoder handles every such block exactly) or whose
+// sub-tables would not fit.
 template <bool DIST>
-SB_DEV bool wave_build(WaveLds &L, int off, int nsym, int toff, int subcap) {
+SB_DEV bool wave_build(WaveLds &L, int off, int nsym, int suboff, int subcap) {
   constexpr int R = DIST ? wd::kDistRoot : wd::kLitRoot;
   const int lane = (int)threadIdx.x;
   uint8_t *lens = L.lens();
   uint16_t *sorted = L.sorted();
-  uint32_t *tab = L.tab + toff;
-  if (lane < 16) L.cnt[lane] = 0;
+  uint32_t *cnt = L.cnt();
+  if (lane < 16) cnt[lane] = 0;
   __syncthreads();
   for (int s = lane; s < nsym; s += 64) {
     const uint32_t l = lens[off + s];
-    if (l) atomicAdd(&L.cnt[l], 1u);
+    if (l) atomicAdd(&cnt[l], 1u);
   }
   __syncthreads();
   CanonW c;
@@ -868,7 +863,7 @@ SB_DEV bool wave_build(WaveLds &L, int off, int nsym, int toff, int subcap) {
   uint32_t code = 0;
   sfor<1, 16>([&](auto I) {
     constexpr int l = decltype(I)::value;
-    const uint32_t k = uni(L.cnt[l]);
+    const uint32_t k = uni(cnt[l]);
     left = 2 * left - (int)k;
     over |= left < 0;
     c.lim[l] = (code + k) << (15 - l);
@@ -900,7 +895,7 @@ SB_DEV bool wave_build(WaveLds &L, int off, int nsym, int toff, int subcap) {
     const uint32_t v = (__builtin_bitreverse32((uint32_t)e) >> (32 - R)) << (15 - R);
     if (v < c.lim[R]) {  // a code of at most R bits
       const uint32_t l = canon_len<R>(c, v);
-      tab[root_slot<R>((uint32_t)e)] = sym_entry(sorted[off + (int)(v >> (15 - l)) + canon_base<R>(c, l)], l, DIST);
+      L.tab[2 * e + DIST] = sym_entry(sorted[off + (int)(v >> (15 - l)) + canon_base<R>(c, l)], l, DIST);
     }
   }
   // sub-tables: one per root prefix of the codes longer than R, sized by the longest code under that prefix
@@ -918,11 +913,12 @@ SB_DEV bool wave_build(WaveLds &L, int off, int nsym, int toff, int subcap) {
     const uint32_t incl = wave_incl_scan(sz);
     const int my = next + (int)(incl - sz);
     if (j < npre && my + (int)sz <= subcap) {
-      tab[root_slot<R>(__builtin_bitreverse32(P) >> (32 - R))] = wd::kSub | (sb << 11) | ((uint32_t)((1 << R) + my) << 16);
+      L.tab[2 * (__builtin_bitreverse32(P) >> (32 - R)) + DIST] =
+          wd::kSub | (sb << 11) | ((uint32_t)(suboff + my) << 16);
       for (uint32_t k = 0; k < sz; k++) {
         const uint32_t v = (P << (15 - R)) | ((__builtin_bitreverse32(k) >> (32 - sb)) << (15 - R - sb));
         const uint32_t l = canon_len(c, v);
-        tab[(1 << R) + my + (int)k] = sym_entry(sorted[off + (int)(v >> (15 - l)) + canon_base(c, l)], l, DIST);
+        L.tab[suboff + my + (int)k] = sym_entry(sorted[off + (int)(v >> (15 - l)) + canon_base(c, l)], l, DIST);
       }
     }
     next += (int)__shfl(incl, 63);
@@ -939,15 +935,9 @@ SB_DEV uint32_t wsym(const WaveLds &L, int wq, int &pos, int st, uint32_t &v) {
   using namespace wd;
   const uint32_t q = (uint32_t)(pos - wq), w = q >> 5;
   const uint32_t lo = __builtin_amdgcn_alignbit(L.win[w + 1], L.win[w], q & 31u);
-  const uint32_t tb = st ? (uint32_t)kDistOff : (uint32_t)kLitOff;
-  const uint32_t R = st ? (uint32_t)kDistRoot : (uint32_t)kLitRoot;
-#ifdef SBAM_TSWZ
-  const uint32_t ri = lo & ((1u << R) - 1u);
-  uint32_t e = L.tab[tb + (ri ^ ((ri >> 5) & (st ? 7u : 15u)))];
-#else
-  uint32_t e = L.tab[tb + (lo & ((1u << R) - 1u))];
-#endif
-  if (e & kSub) e = L.tab[tb + (e >> 16) + ((lo >> R) & ((1u << ((e >> 11) & 31u)) - 1u))];
+  static_assert(kLitRoot == 9 && kDistRoot == 9, "interleaved 9-bit roots");
+  uint32_t e = L.tab[((lo & 511u) << 1) | (uint32_t)st];
+  if (e & kSub) e = L.tab[(e >> 16) + ((lo >> 9) & ((1u << ((e >> 11) & 31u)) - 1u))];
   const uint32_t n = e & 15u, x = (e >> 4) & 15u;
   v = (e >> 16) + __builtin_amdgcn_ubfe(lo, n, x);
   pos += (int)(n + x);
@@ -1194,8 +1184,8 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
     if (h.pos > pend) { ok = false; break; }
     WMARK(0);
     WADD(9, 1);
-    if (!wave_build<true>(L, 288, hdist, kDistOff, kDistSub)) { ok = false; break; }
-    if (!wave_build<false>(L, 0, hlit, kLitOff, kLitSub)) { ok = false; break; }
+    if (!wave_build<true>(L, 288, hdist, kDistSubOff, kDistSub)) { ok = false; break; }
+    if (!wave_build<false>(L, 0, hlit, kLitSubOff, kLitSub)) { ok = false; break; }
     WMARK(1);
 
     // ---- data rounds: 64 segments of kK bits per round
@@ -1714,10 +1704,17 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
     const uint32_t ta2 = tk[tp2 + 2 * lane], tb2 = tk[tp2 + 2 * lane + 1], tn2 = tk[tp2 + 2 * lane + 2];
     const uint64_t farm = __ballot(mt && far);
     uint64_t pend = __ballot(mt);
+    const uint64_t below = (1ull << lane) - 1ull;
+    const int mEnd = mO + Le;
     while (pend) {
       const int f = __ffsll((unsigned long long)pend) - 1;
       const int fr = __builtin_amdgcn_readlane(mO, f);
-      uint64_t ready = pend & __ballot(srcEnd <= fr);
+      // ready: the source ends before the first pending output, or every pending output before this lane's ends
+      // at or before the source starts (pending outputs are disjoint and in lane order, so the nearest one decides)
+      const uint64_t pb = pend & below;
+      const int jn = pb ? 63 - __clzll((long long)pb) : lane;
+      const int endj = __shfl(mEnd, jn);
+      uint64_t ready = pend & __ballot(srcEnd <= fr || pb == 0 || endj <= mO - d);
       if (!((farm >> f) & 1ull)) ready &= ~farm;
       if ((ready >> lane) & 1ull) {
         int done = 0, deff = d;

@@ -650,7 +650,8 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
             p.add_argument("-s", "--spark-bam", action="store_true")
         if name == "full-check":
             p.add_argument("--windows", type=int, default=1,
-                           help="byte-range shards run one after another on one GPU (files larger than HBM)")
+                           help="byte-range shards run one after another on one GPU (files larger than HBM); "
+                                "0 = as many as the file's size, compression ratio and free HBM need")
         if name in ("compute-splits", "count-reads", "full-check"):
             p.add_argument("--gpus", type=int, default=1, help="byte-range shards, one rank per GPU")
             p.add_argument("--dist-backend", default="nccl", help="nccl (RCCL); gloo to rehearse ranks on one GPU")
@@ -667,6 +668,10 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
             else:
                 sys.stdout.write(text)
         return 0
+    if a.cmd == "full-check" and a.windows == 0:
+        from sbam import dist as sdist
+        src, size = sdist.file_source(a.bam)
+        a.windows = sdist.auto_windows(size, src, sdist.device_free_bytes(0), contexts=1)
     if a.cmd == "full-check" and a.windows > 1:
         from sbam import dist as sdist
         parts = sdist.full_check_file(a.bam, a.print_limit, a.intervals, a.reads_to_check, world=a.windows,

@@ -253,6 +253,53 @@ def gather_results(res: ShardResult, plans: Sequence[ShardPlan], device=None) ->
 
 # ---- file-level driver ----------------------------------------------------------------------------------------
 
+# HBM per compressed byte of one loaded range (DESIGN.md §Data layout): the compressed bytes, the uncompressed
+# stream (r per byte, r = uncompressed / compressed), the decoder's token regions (2 r: u16 per uncompressed byte,
+# reserved whole), the success bitmap (r / 8), plus block tables, candidates and the checker's lists (< 0.05).
+def hbm_bytes_per_compressed_byte(ratio: float) -> float:
+    return 1.0 + ratio * (1.0 + 2.0 + 0.125) + 0.05
+
+
+def bgzf_ratio(source: Callable[..., np.ndarray], size: int, sample: int = 8 << 20) -> float:
+    """Uncompressed / compressed bytes over the BGZF blocks of the first `sample` bytes (the block chain from the
+    first header: BSIZE at +16, ISIZE in the block's last 4 bytes — Header.scala, the footer); 3.0 when nothing
+    parses."""
+    buf = source(0, min(size, sample))
+    raw = buf.tobytes()
+    pos = 0  # the first BGZF header (a range may start inside a block): magic 1f 8b 08 04, 'BC' at +12
+    while True:
+        pos = raw.find(b"\x1f\x8b\x08\x04", pos)
+        if pos < 0 or raw[pos + 12:pos + 14] == b"BC":
+            break
+        pos += 1
+    if pos < 0:
+        return 3.0
+    comp = unc = 0
+    while pos + 18 <= buf.size and buf[pos] == 0x1F and buf[pos + 1] == 0x8B:
+        bsize = int(buf[pos + 16]) | (int(buf[pos + 17]) << 8)
+        end = pos + bsize + 1
+        if end > buf.size:
+            break
+        unc += int.from_bytes(buf[end - 4:end].tobytes(), "little")
+        comp += bsize + 1
+        pos = end
+    return unc / comp if comp and unc else 3.0
+
+
+def auto_windows(size: int, source: Callable[..., np.ndarray], free_bytes: int, contexts: int = 2,
+                 headroom: float = 0.8) -> int:
+    """Windows for a `size`-byte range so that `contexts` loaded windows (WindowPipe keeps two) fit in `headroom` of
+    `free_bytes` of HBM, from the file's measured compression ratio (with 10 % margin)."""
+    per_byte = hbm_bytes_per_compressed_byte(1.1 * bgzf_ratio(source, size))
+    need = size * per_byte * contexts
+    return max(1, int(np.ceil(need / (headroom * free_bytes))))
+
+
+def device_free_bytes(device: int) -> int:
+    import torch
+    return int(torch.cuda.mem_get_info(device)[0])
+
+
 def file_source(path: str) -> Tuple[Callable[..., np.ndarray], int]:
     """(source, file size) for a BAM on disk: source(lo, hi[, out]) preads bytes [lo, hi) into a new (or the given)
     uint8 array — a rank touches only its own byte range, never the whole file."""

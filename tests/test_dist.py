@@ -7,7 +7,7 @@ import socket
 import numpy as np
 import pytest
 
-from conftest import fixture_bytes
+from conftest import FIXTURES, fixture_bytes
 
 
 class OracleShard:
@@ -289,3 +289,18 @@ def test_rccl_collectives_single_rank(tmp_path):
     splits, sizes, totals, npos, ns = _expected(name, split_size)
     assert sp == splits and sz == sizes and tot == totals.tolist() and nsucc == ns
     assert golden_ok
+
+
+def test_hbm_budget_and_auto_windows():
+    """HBM per compressed byte (DESIGN.md §Data layout) from the file's measured BGZF ratio; a range that starts
+    inside a block finds the first header; auto_windows fits two contexts in 80 % of the free bytes."""
+    from sbam import dist as sdist
+    src, size = sdist.file_source(os.path.join(FIXTURES, "2.bam"))
+    r = sdist.bgzf_ratio(src, size)
+    assert 2.9 < r < 3.2
+    assert abs(sdist.bgzf_ratio(lambda lo, hi: src(lo + 1000, hi + 1000), size - 1000) - r) < 0.05
+    per = sdist.hbm_bytes_per_compressed_byte(1.1 * r)
+    assert abs(per - (1 + 1.1 * r * 3.125 + 0.05)) < 1e-9
+    need = size * per * 2
+    assert sdist.auto_windows(size, src, int(need / 0.8) + 1) == 1
+    assert sdist.auto_windows(size, src, int(need / 0.8 / 3) + 1) == 3
