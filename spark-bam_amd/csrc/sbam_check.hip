@@ -1108,7 +1108,7 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bi
     // shifts row 0 out and leaves exactly the planes of lanes 256 + t.  The contig-length test reads the length table
     // only at offsets whose int32 is a contig index (a bit loop over that plane: ~1 % of offsets)
     {
-      uint32_t pa = 0, pb = 0, pin = 0, pz = 0, pe = 0, pg = 0;
+      uint32_t pa = 0, pb = 0, pz = 0, pe = 0, pg = 0;
       auto row = [&](int j) {
         const int g = j * kCheckThreads + t;
         const uint32_t W0 = w32[g], W1 = w32[g + 1];
@@ -1118,13 +1118,13 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bi
           const uint32_t by = (uint32_t)I & 0xffu;
           pa = push_bit(pa, I < -1);
           pb = push_bit(pb, I >= nref);
-          pin = push_bit(pin, (uint32_t)I < (uint32_t)nref);
           pz = push_bit(pz, by == 0);
           pe = push_bit(pe, by == 1);
           pg = push_bit(pg, by > 64);
         }
       };
-      // I(y + 4) > len[I(y)] where I(y) is a contig index; r0: the row of plane bit 31 (1 for lanes 256 + t)
+      // I(y + 4) > len[I(y)] where I(y) is a contig index: the bits of neither plane (-1 <= I < n_ref; I = -1
+      // is tested and skipped); r0: the row of plane bit 31 (1 for lanes 256 + t)
       auto bigpos = [&](uint32_t in, int r0) {
         uint32_t pc = 0;
         for (uint32_t q = in; q; q &= q - 1u) {
@@ -1132,7 +1132,7 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bi
           const int y = 4 * (((k >> 2) + r0) * kCheckThreads + t) + (k & 3);
           const int32_t I = (int32_t)__builtin_amdgcn_alignbyte(w32[(y >> 2) + 1], w32[y >> 2], y & 3);
           const int32_t I4 = (int32_t)__builtin_amdgcn_alignbyte(w32[(y >> 2) + 2], w32[(y >> 2) + 1], y & 3);
-          pc |= I4 > s_lens[I] ? (1u << b) : 0u;
+          pc |= (I >= 0 && I4 > s_lens[I >= 0 ? I : 0]) ? (1u << b) : 0u;
         }
         return pc;
       };
@@ -1140,7 +1140,7 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bi
       for (int j = 0; j < 8; j++) row(j);
       s_pl[0][t] = pa;
       s_pl[1][t] = pb;
-      s_pl[2][t] = bigpos(pin, 0);
+      s_pl[2][t] = bigpos(~(pa | pb), 0);
       s_pl[3][t] = pz;
       s_pl[4][t] = pe;
       s_pl[5][t] = pg;
@@ -1148,7 +1148,7 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bi
         row(8);
         s_pl[0][kCheckThreads + t] = pa;
         s_pl[1][kCheckThreads + t] = pb;
-        s_pl[2][kCheckThreads + t] = bigpos(pin, 1);
+        s_pl[2][kCheckThreads + t] = bigpos(~(pa | pb), 1);
         s_pl[3][kCheckThreads + t] = pz;
         s_pl[4][kCheckThreads + t] = pe;
         s_pl[5][kCheckThreads + t] = pg;

@@ -1133,15 +1133,27 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         // packed: advance (5 bits) | repeat (8) | value (4) | value is "previous" (1)
         const uint32_t info = (l + xb) | (rep << 5) | ((sym < 16 ? sym : 0u) << 13) | ((sym == 16 ? 1u : 0u) << 17);
         // the true chain through the 64 decoded offsets: only the offsets and the running count are serial
-        // (scalar: one readlane per symbol); values, repeat targets and LDS writes follow for all members at once
+        // (scalar readlanes); values, repeat targets and LDS writes follow for all members at once.  info2 = the
+        // info of the symbol after this lane's (a shuffle), so one walk step takes two symbols: two independent
+        // readlanes per step instead of one dependent readlane per symbol.
+        const uint32_t nx = (uint32_t)lane + (info & 31u);
+        const uint32_t info2 = (uint32_t)__shfl((int)info, (int)min(nx, 63u));
         int o = 0;
         uint64_t chain = 0;
         const int n0 = n;
         while (o < 64 && n < total) {
           const uint32_t in = (uint32_t)__builtin_amdgcn_readlane((int)info, o);
+          const uint32_t in2 = (uint32_t)__builtin_amdgcn_readlane((int)info2, o);
           chain |= 1ull << o;
           n += (int)((in >> 5) & 255u);
-          o += (int)(in & 31u);
+          const int o1 = o + (int)(in & 31u);
+          if (o1 < 64 && n < total) {
+            chain |= 1ull << o1;
+            n += (int)((in2 >> 5) & 255u);
+            o = o1 + (int)(in2 & 31u);
+          } else {
+            o = o1;
+          }
         }
         o = uni(o);
         n = uni(n);
