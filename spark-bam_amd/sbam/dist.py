@@ -23,6 +23,8 @@ one rank's range through two contexts in windows (CanLoadBam.scala:281-334 at mo
 from __future__ import annotations
 
 import os
+import sys
+import time
 from dataclasses import dataclass
 from typing import Callable, List, Optional, Sequence, Tuple
 
@@ -589,10 +591,14 @@ class WindowPipe:
             staged = {g: self.stager.submit(self._stage, g) for g in range(g0, g0 + min(2, W))}
             fut = None
         sh = self._load(g0, staged[g0]) if fut is None else None
+        dbg = os.environ.get("SBAM_PIPE_DEBUG")
         for w in range(W):
             g = g0 + w
+            t0 = time.perf_counter()
             if sh is None:
                 sh = fut.result()
+            if dbg:
+                print(f"[pipe] window {g}: waited {1e3 * (time.perf_counter() - t0):.1f} ms for its load", file=sys.stderr)
             last = w + 1 == W
             if not last or self.prefetch:
                 if g + 1 not in staged:
@@ -600,7 +606,10 @@ class WindowPipe:
                 fut = self.loader.submit(self._load, g + 1, staged[g + 1])
             if (w + 2 < W or self.prefetch) and g + 2 not in staged:
                 staged[g + 2] = self.stager.submit(self._stage, g + 2)
+            t1 = time.perf_counter()
             out.append(self.run_window(sh))
+            if dbg:
+                print(f"[pipe] window {g}: ran {1e3 * (time.perf_counter() - t1):.1f} ms", file=sys.stderr)
             sh = None
         self.g = g0 + W
         if self.prefetch:
