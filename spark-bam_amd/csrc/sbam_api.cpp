@@ -39,6 +39,10 @@ struct sbam_ctx {
   size_t cc_cap = 0, coff_cap = 0;
   Candidate *d_slots = nullptr;  // one-pass scan: kScanSlots per chunk
   size_t slots_cap = 0;
+  // per-call query scratch (split starts / answers): kept, since hipMalloc + hipFree per call cost ~0.5 ms of
+  // host time each (a device-wide synchronisation) between the kernels of a step
+  int64_t *d_qa = nullptr, *d_qb = nullptr;
+  size_t qa_cap = 0, qb_cap = 0, lens_cap = 0;
   // block table (relative offsets), device + host
   int64_t nblocks = -1;
   int64_t *d_bstart = nullptr, *d_buoff = nullptr;
@@ -262,6 +266,8 @@ void sbam_close(sbam_ctx *c) {
   dfree(c->d_cc);
   dfree(c->d_coff);
   dfree(c->d_slots);
+  dfree(c->d_qa);
+  dfree(c->d_qb);
   dfree(c->d_status);
   dfree(c->d_found);
   dfree(c->d_bstart);
@@ -389,15 +395,13 @@ int sbam_find_block_starts(sbam_ctx *c, const int64_t *starts, int64_t n, int32_
     rel[i] = starts[i] - c->base;
     if (rel[i] < 0 || rel[i] > c->D) return set_err(c, SBAM_ERR_ARG, "split start %lld outside loaded bytes", (long long)starts[i]);
   }
-  int64_t *d_q = nullptr, *d_o = nullptr;
-  HIPCHK(c, dalloc(&d_q, n));
-  HIPCHK(c, dalloc(&d_o, n));
+  HIPCHK(c, ensure(&c->d_qa, &c->qa_cap, (size_t)n));
+  HIPCHK(c, ensure(&c->d_qb, &c->qb_cap, (size_t)n));
+  int64_t *d_q = c->d_qa, *d_o = c->d_qb;
   HIPCHK(c, hipMemcpyAsync(d_q, rel.data(), n * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, launch_find_block_starts(c->d_comp, c->D, c->d_cand, c->ncand, d_q, n, nchk, d_o, c->stream));
   HIPCHK(c, hipMemcpyAsync(out, d_o, n * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  dfree(d_q);
-  dfree(d_o);
   for (int64_t i = 0; i < n; i++) {
     if (out[i] < 0) {
       // HeaderSearchFailedException(path, start, positionsAttempted = MAX_BLOCK_SIZE) (FindBlockStart.scala:16-35)
@@ -610,9 +614,9 @@ int sbam_offset_to_pos(sbam_ctx *c, int64_t off, sbam_pos *p) {
 int sbam_set_contig_lengths(sbam_ctx *c, int32_t n_ref, const int64_t *lengths) {
   if (!c || n_ref < 0 || (n_ref && !lengths)) return SBAM_ERR_ARG;
   HIPCHK(c, hipSetDevice(c->device));
-  dfree(c->d_lens);
-  HIPCHK(c, dalloc(&c->d_lens, n_ref));
-  if (n_ref) HIPCHK(c, hipMemcpy(c->d_lens, lengths, n_ref * 8, hipMemcpyHostToDevice));
+  HIPCHK(c, ensure(&c->d_lens, &c->lens_cap, (size_t)n_ref));
+  if (n_ref) HIPCHK(c, hipMemcpyAsync(c->d_lens, lengths, n_ref * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   c->h_lens.assign(lengths, lengths + n_ref);
   c->nref = n_ref;
   c->bm_valid = false;
@@ -827,9 +831,9 @@ static int find_record_starts(sbam_ctx *c, const std::vector<int64_t> &x0, int32
   const int64_t n = (int64_t)x0.size();
   out.assign(n, -1);
   if (!n) return SBAM_OK;
-  int64_t *d_x = nullptr, *d_o = nullptr;
-  HIPCHK(c, dalloc(&d_x, n));
-  HIPCHK(c, dalloc(&d_o, n));
+  HIPCHK(c, ensure(&c->d_qa, &c->qa_cap, (size_t)n));
+  HIPCHK(c, ensure(&c->d_qb, &c->qb_cap, (size_t)n));
+  int64_t *d_x = c->d_qa, *d_o = c->d_qb;
   HIPCHK(c, hipMemcpyAsync(d_x, x0.data(), n * 8, hipMemcpyHostToDevice, c->stream));
   const bool bm = use_bm && c->bm_valid && c->bm_R == R;
   {
@@ -839,8 +843,6 @@ static int find_record_starts(sbam_ctx *c, const std::vector<int64_t> &x0, int32
   }
   HIPCHK(c, hipMemcpyAsync(out.data(), d_o, n * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  dfree(d_x);
-  dfree(d_o);
   return SBAM_OK;
 }
 
