@@ -113,8 +113,10 @@ SB_DEV uint32_t ref_err(int32_t ri, int32_t rp, const int32_t *lensL, const int6
 
 // (l_seq + 1) / 2 + l_seq and 32 + l_read_name + 4 n_cigar + that, in Java Int (wrap, '/' toward zero)
 SB_DEV bool too_few_remaining(int32_t bs, int32_t lrn, int32_t nc, int32_t ls) {
-  const int32_t t = (int32_t)((uint32_t)ls + 1u);
-  const int32_t nsq = (int32_t)((uint32_t)(t / 2) + (uint32_t)ls);
+  // (ls + 1) / 2 truncated toward zero (Int division) = (ls + 1 + [ls < -1]) >> 1, arithmetic, also across the
+  // int32 wrap at ls = INT_MAX: a compare and a carry-in add instead of a sign extract, an add and a shift
+  const int32_t half = (int32_t)((uint32_t)ls + 1u + (ls < -1 ? 1u : 0u)) >> 1;
+  const int32_t nsq = (int32_t)((uint32_t)half + (uint32_t)ls);
   const int32_t implied = (int32_t)(32u + (uint32_t)lrn + 4u * (uint32_t)nc + (uint32_t)nsq);
   return bs < implied;
 }

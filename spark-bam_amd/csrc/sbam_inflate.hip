@@ -738,8 +738,11 @@ constexpr int kLitRoot = 9, kDistRoot = 9;
 constexpr int kLitSub = 340, kDistSub = 80;  // ENOUGH - root: 852 - 512 and 592 - 512 at root 9
 constexpr int kLitSubOff = 2 << kLitRoot, kDistSubOff = kLitSubOff + kLitSub;
 constexpr int kTab = kDistSubOff + kDistSub;
-constexpr int kCp = 12;            // checkpoints per lane
-constexpr int kCpSteps = 8;        // symbols between checkpoints
+#ifndef SBAM_CP  // (8 × 12 and 16 × 6 symbols: within 0.2 ms of 12 × 8)
+#define SBAM_CP 12
+#endif
+constexpr int kCp = SBAM_CP;                // checkpoints per lane
+constexpr int kCpSteps = 96 / SBAM_CP;      // symbols between checkpoints
 // Lanes > 0 start decoding kWarm bits before their segment, so that by the segment start their path has usually
 // resynchronised with the true one: the first symbol boundary at or after the segment start ("entry") then equals
 // the left neighbour's exit and phase A's counts from the entry on need no phase-B re-decode.  Decode at 10 GB:
@@ -752,24 +755,26 @@ constexpr int kCpSteps = 8;        // symbols between checkpoints
 constexpr int kWarm = SBAM_WARM;
 // Phase A keeps the tokens of its first kTR symbol steps in registers (two per VGPR, step j in half j & 1 of
 // tr[j / 2]: the steps are unrolled, so every index is static).  A lane whose phase-A path is the true one (the
-// common case after the warm-up) then only stores them in phase C; it decodes again only past step kTR.
+// common case after the warm-up) then only stores them in phase C; it decodes again only past step kTR.  With the
+// round-3 v2 step (38 VALU instead of 58) the register budget is what limits kTR: 96 tokens spilled 48 VGPRs to
+// scratch, 80 spill 11 (decode at 10 GB: 96 → 47.7 ms, 80 → 45.9; 72: 47.5, its phase C re-decodes more tails).
 #ifndef SBAM_TR
-#define SBAM_TR 96
+#define SBAM_TR 80
 #endif
 constexpr int kTR = SBAM_TR;
 static_assert(kTR % 2 == 0 && kTR <= kCp * kCpSteps, "register tokens come from the unrolled checkpoint steps");
 constexpr int kScratchDw = 256;    // window tail that doubles as header / table-build scratch
-constexpr uint32_t kSub = 1u << 10;  // table entry flag: pointer to a sub-table
 // a block header (<= 3 + 14 + 57 + 320 * 14 bits) plus the window's start alignment fits before the scratch
 static_assert(128 + 3 + 14 + 57 + 320 * 14 + 64 <= (kWinDw - kScratchDw) * 32, "header fits the window");
-enum : uint32_t { K_LIT = 0, K_LEN = 1, K_DIST = 2, K_SPEC = 3 };
+enum : uint32_t { K_LIT = 0, K_LEN = 1, K_DIST = 2, K_SPEC = 3, K_SUBP = 4 };  // K_SUBP: a sub-table pointer
 enum : int { ST_NONE = 0, ST_EOB = 1, ST_ERR = 2, ST_OUT = 3 };
 }  // namespace wd
 
-// Table entry (u32): bits 0-3 code length, 4-7 extra bits, 8-9 kind, 10 sub-table flag, 11-15 sub-table index
-// bits, 16-31 value in token form, so that value + extra bits is the symbol's u16 token (literal byte; 253 + length
-// base; 0x7fff + distance base; K_SPEC: 0 = end of block, 1 = invalid symbol; for a sub-table pointer: the
-// sub-table's offset in the alphabet's table).
+// Table entry (u32): bits 0-3 code length, 4-7 extra bits, byte 1 the kind (alone in its byte, so a kind test is one
+// byte-select compare), 16-31 value in token form, so that value + extra bits is the symbol's u16 token (literal
+// byte; 253 + length base; 0x7fff + distance base; K_SPEC: 0 = end of block, 1 = invalid symbol).  A sub-table
+// pointer (kind K_SUBP): bits 0-4 the sub-table's index bits (a bit-field width as it stands), 16-31 the sub-table's
+// byte offset in tab.
 struct WaveLds {
   uint32_t win[wd::kWinDw];
   uint32_t tab[wd::kTab];
@@ -825,7 +830,6 @@ SB_DEV int32_t canon_base(const CanonW &c, uint32_t l) {  // c.base[l] by select
 SB_DEV uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 SB_DEV int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 SB_DEV uint64_t uni(uint64_t x) { return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x); }
-
 // Inclusive prefix sum over the wave: row_shr 1/2/4/8 within rows of 16, then row_bcast 15 / 31 across rows
 // (DPP: no LDS round trip).
 SB_DEV uint32_t wave_incl_scan(uint32_t x) {
@@ -914,7 +918,7 @@ SB_DEV bool wave_build(WaveLds &L, int off, int nsym, int suboff, int subcap) {
     const int my = next + (int)(incl - sz);
     if (j < npre && my + (int)sz <= subcap) {
       L.tab[2 * (__builtin_bitreverse32(P) >> (32 - R)) + DIST] =
-          wd::kSub | (sb << 11) | ((uint32_t)(suboff + my) << 16);
+          (wd::K_SUBP << 8) | sb | ((uint32_t)(4 * (suboff + my)) << 16);
       for (uint32_t k = 0; k < sz; k++) {
         const uint32_t v = (P << (15 - R)) | ((__builtin_bitreverse32(k) >> (32 - sb)) << (15 - R - sb));
         const uint32_t l = canon_len(c, v);
@@ -927,21 +931,31 @@ SB_DEV bool wave_build(WaveLds &L, int off, int nsym, int suboff, int subcap) {
   return next <= subcap;
 }
 
-// One symbol of the alphabet `st` selects (literal/length, or distance after a length) at bit position pos of the
-// staged window (positions are bits from the block's 16-B aligned base; wq = the window's first bit): 32 bits of
-// lookahead from two window dwords, the root entry, the sub-table entry for long codes, the extra bits.  Advances
-// pos; returns the entry, v = the symbol's token (literal byte, 253 + length, 0x7fff + distance) or K_SPEC value.
-SB_DEV uint32_t wsym(const WaveLds &L, int wq, int &pos, int st, uint32_t &v) {
+// LDS byte address of a pointer into __shared__ memory
+SB_DEV uint32_t lds_addr(const void *p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+
+// One symbol of the alphabet the state st4 selects (0: literal/length, 4: distance after a length) at bit position
+// pos (bits from the block's 16-B aligned base; wp = the staged window less its first bit's dword, so wp[pos >> 5]
+// holds bit pos): 32 bits of lookahead from two window dwords, the root entry at byte (bits & 511) << 3 | st4 of
+// tab, the sub-table entry for long codes, the extra bits.  Advances pos; returns the kind, v = the symbol's token
+// (literal byte, 253 + length, 0x7fff + distance) or K_SPEC value.
+SB_DEV uint32_t wsym(const uint32_t *wp, const WaveLds &L, int &pos, uint32_t st4, uint32_t &v) {
   using namespace wd;
-  const uint32_t q = (uint32_t)(pos - wq), w = q >> 5;
-  const uint32_t lo = __builtin_amdgcn_alignbit(L.win[w + 1], L.win[w], q & 31u);
+  uint32_t a;  // LDS byte address of wp[pos >> 5]
+  asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(a) : "v"((uint32_t)pos >> 5), "s"(lds_addr(wp)));
+  const auto *q = reinterpret_cast<const __attribute__((address_space(3))) uint32_t *>((uintptr_t)a);
+  const uint32_t lo = __builtin_amdgcn_alignbit(q[1], q[0], (uint32_t)pos);  // (the shift is pos & 31)
   static_assert(kLitRoot == 9 && kDistRoot == 9, "interleaved 9-bit roots");
-  uint32_t e = L.tab[((lo & 511u) << 1) | (uint32_t)st];
-  if (e & kSub) e = L.tab[(e >> 16) + ((lo >> 9) & ((1u << ((e >> 11) & 31u)) - 1u))];
+  const char *tb = reinterpret_cast<const char *>(L.tab);
+  uint32_t e = *reinterpret_cast<const uint32_t *>(tb + (((lo << 3) & 0xff8u) | st4));
+  if (((e >> 8) & 0xffu) == K_SUBP)
+    e = *reinterpret_cast<const uint32_t *>(tb + (e >> 16) + 4u * __builtin_amdgcn_ubfe(lo, 9u, e));
   const uint32_t n = e & 15u, x = (e >> 4) & 15u;
   v = (e >> 16) + __builtin_amdgcn_ubfe(lo, n, x);
   pos += (int)(n + x);
-  return e;
+  return (e >> 8) & 0xffu;
 }
 
 // Wave-uniform bit reader for block headers.
@@ -1206,6 +1220,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       const int Sp = (int)(S >> 10);
       wq = (Sp >> 7) << 7;
       wave_stage(L.win, base, base_dw, wq >> 5, lim_dw);
+      const uint32_t *wp = L.win - (wq >> 5);  // wp[pos >> 5]: the staged dword holding bit pos
       WMARK(2);
       WADD(6, 1);
       const int seg_start = lane == 0 ? Sp : Sp + lane * kK;
@@ -1223,7 +1238,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       uint32_t stR = 0, bytR = 0;  // state (exit key) and bytes after step kTR
       int slack = 1 << 30;  // min over the phase-A path's distances of (local bytes before the match - distance)
       {
-        int stt = lane == 0 ? (int)((S >> 9) & 1) : 0;
+        uint32_t st4 = lane == 0 ? (S >> 7) & 4u : 0u;  // state << 2 (the table's byte offset for the state)
         uint32_t pl = lane == 0 ? (S & 511u) : 0u;
         int rp = seg_start;  // reader position
         bool go = true;
@@ -1236,18 +1251,23 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
           rp = seg_start - kWarm;
           if (rp <= Sp) {  // from the round's true start, in its true state
             rp = Sp;
-            stt = (int)((S >> 9) & 1);
+            st4 = (S >> 7) & 4u;
             pl = S & 511u;
           }
           while (rp < seg_start) {
             uint32_t v;
-            const uint32_t kind = (wsym(L, wq, rp, stt, v) >> 8) & 3u;
+            const uint32_t kind = wsym(wp, L, rp, st4, v);
             pl = kind == K_LEN ? v - 253u : pl;
-            stt = kind == K_LEN ? 1 : 0;
+            st4 = kind == K_LEN ? 4u : 0u;
           }
         }
         WMARK(13);
-        entry = ((uint32_t)rp << 10) | ((uint32_t)stt << 9) | pl;
+        entry = ((uint32_t)rp << 10) | (st4 << 7) | pl;
+        // 0x7fff + local bytes before the pending match (a distance d = token - 0x7fff is too far back for the path
+        // when this minus the token is below -o0)
+        uint32_t bq = 0x7fffu - pl;
+        bool first = nst == 0;  // no stop yet
+        const bool chk = out < 32768;  // o0 >= out, and a distance is at most 32768
         // one symbol, predicated: a lane that is done (stopped out of the data, or past its segment) decodes the
         // same symbol again and commits nothing, so the steps need no exec-mask branches
         // ST: the step's index when it is below kTR (its token goes to tr), else -1
@@ -1257,10 +1277,10 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
           const uint32_t p0 = (uint32_t)rp;
           int rq = rp;
           uint32_t v;
-          const uint32_t kind = (wsym(L, wq, rq, stt, v) >> 8) & 3u;
+          const uint32_t kind = wsym(wp, L, rq, st4, v);
           const bool outp = rq > pend;
           const bool stp = live && (kind == K_SPEC || outp);
-          if (__ballot(stp) != 0) {  // rare: record the stop (exit in the literal state | kind) and decode on
+          if (__builtin_amdgcn_ballot_w64(stp) != 0) {  // rare: record the stop (exit in the literal state | kind) and decode on
             const uint32_t ek = ((uint32_t)rq << 10) | (uint32_t)(outp ? ST_OUT : v == 0 ? ST_EOB : ST_ERR);
             const uint32_t cn = tokA | (bytA << 12);
             const bool w1 = stp && nst == 0, w2 = stp && nst == 1;
@@ -1271,6 +1291,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
             s2e = w2 ? ek : s2e;
             s2c = w2 ? cn : s2c;
             nst += stp ? 1 : 0;
+            first = first && !stp;
             go = (stp && outp) ? false : go;
           }
           rp = live ? rq : rp;
@@ -1282,26 +1303,26 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
               tr[sj / 2] = __builtin_amdgcn_perm(v, tr[sj / 2], 0x05040100u);  // low half kept, v above
             }
           }
-          // selects only (no exec-mask branches): counts, pending length, and the path's distance check (zlib
-          // "invalid distance too far back") up to its first stop
-          const uint32_t cm = cnt ? ~0u : 0u;  // used by every lane (a select on cnt becomes a branch)
-          const bool isLen = kind == K_LEN;
+          // selects and carry-in adds only (no exec-mask branches): counts, pending length, and the path's distance
+          // check (zlib "invalid distance too far back") up to its first stop
+          const bool cl = cnt && kind == K_LEN;
           const uint32_t lenv = v - 253u;
-          const uint32_t nb = kind == K_LIT ? 1u : (isLen ? lenv : 0u);
-          const int sx = (int)bytA - (int)pl - (int)(v - 0x7fffu);
-          const int sv = (int)((cm & (uint32_t)sx) | (~cm & (1u << 30)));  // v_bfi
-          slack = min(slack, (nst == 0 && kind == K_DIST) ? sv : (1 << 30));
-          tokA -= cm;
-          bytA += nb & cm;
-          pl = (isLen & cnt) ? lenv : pl;
-          stt = live ? (int)(cnt & isLen) : stt;
+          if (chk) {  // (wave-uniform: from 32 KiB of block output on, no distance reaches back past its start)
+            const int sx = min(slack, (int)(bq - v));
+            slack = (cnt && first && kind == K_DIST) ? sx : slack;
+            bq = cl ? bytA + 0x7fffu : bq;
+          }
+          tokA += cnt ? 1u : 0u;                                        // (v_addc with the lane mask as carry-in)
+          bytA += (cl ? lenv : 0u) + ((cnt && kind == K_LIT) ? 1u : 0u);  // + length, or + 1 for a literal
+          pl = cl ? lenv : pl;
+          st4 = live ? (cl ? 4u : 0u) : st4;
         };
         // checkpoints every kCpSteps steps (wave-uniform, so a record costs no divergent branch): the lane's
         // position if it is at a literal/length boundary
         sfor<0, kCp>([&](auto J) {
           constexpr int jj = decltype(J)::value;
           const bool live = go && rp < seg_end;
-          cp[jj] = (live && stt == 0) ? (uint32_t)rp : ~0u;
+          cp[jj] = (live && st4 == 0) ? (uint32_t)rp : ~0u;
           cc[jj] = tokA | (bytA << 12);
           if (__ballot(live) != 0) {
             if constexpr (jj * kCpSteps < kTR) {
@@ -1315,12 +1336,12 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
             }
           }
           if constexpr ((jj + 1) * kCpSteps == kTR) {
-            stR = ((uint32_t)rp << 10) | ((uint32_t)stt << 9) | pl;
+            stR = ((uint32_t)rp << 10) | (st4 << 7) | pl;
             bytR = bytA;
           }
         });
         while (__ballot(go && rp < seg_end) != 0) step(std::integral_constant<int, -1>{});
-        exitEnd = ((uint32_t)rp << 10) | ((uint32_t)stt << 9) | pl;
+        exitEnd = ((uint32_t)rp << 10) | (st4 << 7) | pl;
       }
       WMARK(3);
       // the lane's result if its guessed start is the true one: the path ends at its first stop
@@ -1355,7 +1376,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         if (__ballot(need || upd) == 0) break;
         WADD(7, 1);
         if (need) {
-          int stt = (int)((pex >> 9) & 1);
+          uint32_t st4 = (pex >> 7) & 4u;
           uint32_t pl = pex & 511u, tk = 0, by = 0;
           int rp = (int)(pex >> 10);
           // the first checkpoint at or after the reader
@@ -1370,7 +1391,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
           uint32_t tcp = next_cp((uint32_t)rp);
           mode = kModeF;
           for (;;) {
-            if (stt == 0 && (uint32_t)rp == tcp) {  // on the first-pass path from here
+            if (st4 == 0 && (uint32_t)rp == tcp) {  // on the first-pass path from here
               uint32_t cj = 0, sj = 0;
               sfor<0, kCp>([&](auto I) {
                 const bool hit = cp[decltype(I)::value] == tcp;
@@ -1400,11 +1421,11 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
               mode = kModeF;
             }
             if (rp >= seg_end) {
-              res = SegResult{tk, by, ((uint32_t)rp << 10) | ((uint32_t)stt << 9) | pl, ST_NONE, false};
+              res = SegResult{tk, by, ((uint32_t)rp << 10) | (st4 << 7) | pl, ST_NONE, false};
               break;
             }
             uint32_t v;
-            const uint32_t kind = (wsym(L, wq, rp, stt, v) >> 8) & 3u;
+            const uint32_t kind = wsym(wp, L, rp, st4, v);
             const bool outp = rp > pend;
             if (kind == K_SPEC || outp) {
               res = SegResult{tk, by, (uint32_t)rp << 10, outp ? ST_OUT : v == 0 ? ST_EOB : ST_ERR, false};
@@ -1413,7 +1434,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
             tk++;
             by += kind == K_LIT ? 1u : kind == K_LEN ? v - 253u : 0u;
             pl = kind == K_LEN ? v - 253u : pl;
-            stt = kind == K_LEN ? 1 : 0;
+            st4 = kind == K_LEN ? 4u : 0u;
             if ((uint32_t)rp > tcp) tcp = next_cp((uint32_t)rp);
           }
           nxt = res.stop != ST_NONE ? res.exit : res.exit;
@@ -1459,17 +1480,17 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         uint32_t ti = (uint32_t)ntok + (itok - my_tok);
         // decode from key st until the reader reaches endp (or the end-of-block symbol of lane f), writing tokens
         auto run = [&](uint32_t st, int endp) {
-          int stt = (int)((st >> 9) & 1);
+          uint32_t st4 = (st >> 7) & 4u;
           uint32_t pl = st & 511u;
           int rp = (int)(st >> 10);
           while (rp < endp) {
             uint32_t v;
-            const uint32_t kind = (wsym(L, wq, rp, stt, v) >> 8) & 3u;
+            const uint32_t kind = wsym(wp, L, rp, st4, v);
             if (kind == K_SPEC) break;
             if (kind == K_DIST) derr |= (int)(v - 0x7fffu) > o - (int)pl;  // v: the token
             o += kind == K_LIT ? 1 : kind == K_LEN ? (int)v - 253 : 0;
             pl = kind == K_LEN ? v - 253u : pl;
-            stt = kind == K_LEN ? 1 : 0;
+            st4 = kind == K_LEN ? 4u : 0u;
             *reinterpret_cast<uint16_t *>(reg + 2 * ti) = (uint16_t)v;
             ti++;
           }
