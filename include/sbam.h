@@ -98,6 +98,13 @@ void sbam_close(sbam_ctx *ctx);
  * of the same file (base_offset > 0 and the same file_size); otherwise sbam_header / sbam_set_contig_lengths
  * must run again before a check. */
 int sbam_load(sbam_ctx *ctx, const uint8_t *data, int64_t len, int64_t base_offset, int64_t file_size);
+/* Size a context's device buffers for windows of up to comp_bytes compressed bytes, n_blocks BGZF blocks,
+ * ubytes uncompressed bytes and n_records records (0: leave the record-sized buffers alone), so that no later
+ * sbam_load / stage reallocates: the buffers are grow-only, and growing one is a hipFree + hipMalloc of up to
+ * tens of GB that synchronises the device (a streamed Spark task whose next split range is larger than any
+ * before it).  Allocates nothing that is already large enough.  (No reference counterpart: the JVM channel has
+ * no device memory; CanLoadBam.scala:281-334 re-opens a channel per split.) */
+int sbam_reserve(sbam_ctx *ctx, int64_t comp_bytes, int64_t n_blocks, int64_t ubytes, int64_t n_records);
 const sbam_error *sbam_last_error(const sbam_ctx *ctx);
 /* The path (Path.toString) that exception messages name, as the reference's HeaderSearchFailedException /
  * NoReadFoundException format it (HeaderSearchFailedException.scala:7-12, FindRecordStart.scala:66-71);

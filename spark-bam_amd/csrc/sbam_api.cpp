@@ -123,10 +123,20 @@ void dfree(T *&p) {
   if (p) (void)hipFree(p);
   p = nullptr;
 }
+// SBAM_LOG_GROW=1: report every reallocation of an existing buffer (the streamed pipe's stalls)
+bool log_grow() {
+  static const bool on = [] {
+    const char *e = std::getenv("SBAM_LOG_GROW");
+    return e && *e && *e != '0';
+  }();
+  return on;
+}
 // grow-only device buffer: reused across sbam_reset() so a re-run allocates nothing
 template <class T>
 hipError_t ensure(T **p, size_t *cap, size_t n) {
   if (*p && *cap >= n) return hipSuccess;
+  if (*p && log_grow())
+    std::fprintf(stderr, "[sbam] grow %zu -> %zu bytes\n", *cap * sizeof(T), std::max<size_t>(n, 1) * sizeof(T));
   dfree(*p);
   *cap = 0;
   hipError_t e = dalloc(p, n);
@@ -219,6 +229,7 @@ sbam_pos pos_of(const sbam_ctx *c, int64_t x) {
 int ensure_bitmap(sbam_ctx *c, int64_t x0, int64_t x1) {
   const size_t words = (size_t)((x1 - (x0 & ~(int64_t)63) + 63) / 64) + 1;
   if (words > c->bitmap_cap) {
+    if (c->d_bitmap && log_grow()) std::fprintf(stderr, "[sbam] grow bitmap %zu -> %zu words\n", c->bitmap_cap, words);
     dfree(c->d_bitmap);
     HIPCHK(c, dalloc(&c->d_bitmap, words));
     c->bitmap_cap = words;
@@ -336,6 +347,45 @@ int sbam_load(sbam_ctx *c, const uint8_t *data, int64_t len, int64_t base_offset
   c->base = base_offset;
   c->file_size = file_size;
   return sbam_reset(c);
+}
+
+int sbam_reserve(sbam_ctx *c, int64_t comp_bytes, int64_t n_blocks, int64_t ubytes, int64_t n_records) {
+  if (!c || comp_bytes < 0 || n_blocks < 0 || ubytes < 0 || n_records < 0) return SBAM_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (comp_bytes > c->D) {  // keep the resident bytes (sbam_load replaces them anyway)
+    uint8_t *p = nullptr;
+    HIPCHK(c, dalloc(&p, (size_t)comp_bytes + kCompPad));
+    if (c->D + kCompPad > 0) HIPCHK(c, hipMemcpy(p, c->d_comp, (size_t)c->D + kCompPad, hipMemcpyDeviceToDevice));
+    dfree(c->d_comp);
+    c->d_comp = p;
+    c->comp_cap = (size_t)comp_bytes + kCompPad;
+  }
+  const int64_t nchunks = (comp_bytes + kScanChunk - 1) / kScanChunk;
+  HIPCHK(c, ensure(&c->d_cc, &c->cc_cap, nchunks));
+  HIPCHK(c, ensure(&c->d_coff, &c->coff_cap, nchunks));
+  HIPCHK(c, ensure(&c->d_slots, &c->slots_cap, (size_t)nchunks * kScanSlots));
+  // candidates: every block's header plus the rare false positives inside payloads
+  HIPCHK(c, ensure(&c->d_cand, &c->cand_cap, (size_t)(n_blocks + n_blocks / 8 + 1024)));
+  HIPCHK(c, ensure(&c->d_bstart, &c->bcap[0], n_blocks + 1));
+  HIPCHK(c, ensure(&c->d_bh, &c->bcap[1], n_blocks + 1));
+  HIPCHK(c, ensure(&c->d_bc, &c->bcap[2], n_blocks + 1));
+  HIPCHK(c, ensure(&c->d_bu, &c->bcap[3], n_blocks + 1));
+  HIPCHK(c, ensure(&c->d_buoff, &c->bcap[4], n_blocks + 1));
+  HIPCHK(c, ensure(&c->d_u, &c->u_cap, (size_t)ubytes + kStreamPad));
+  HIPCHK(c, ensure(&c->d_status, &c->status_cap, n_blocks));
+  HIPCHK(c, ensure(&c->d_found, &c->found_cap, n_blocks));
+  HIPCHK(c, ensure(&c->d_pool, &c->pool_cap, inflate_token_bytes(ubytes, n_blocks)));
+  HIPCHK(c, ensure(&c->d_slow, &c->slow_cap, n_blocks));
+  if (int rc = ensure_bitmap(c, 0, ubytes)) return rc;
+  if (n_records > 0) {  // the chain pass's PASS0 list (about one entry per record) and loadReads' offsets
+    const size_t n = (size_t)(n_records + n_records / 8 + 4096);
+    HIPCHK(c, ensure(&c->d_plist, &c->plist_cap, n));
+    HIPCHK(c, ensure(&c->d_pfb, &c->pfb_cap, n));
+    HIPCHK(c, ensure(&c->d_pok, &c->pok_cap, n));
+    HIPCHK(c, ensure(&c->d_roff, &c->roff_cap, n));
+  }
+  return SBAM_OK;
 }
 
 int sbam_reset(sbam_ctx *c) {

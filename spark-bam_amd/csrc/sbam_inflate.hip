@@ -761,6 +761,9 @@ constexpr int kWarm = SBAM_WARM;
 // common case after the warm-up) then only stores them in phase C; it decodes again only past step kTR.  With the
 // round-3 v2 step (38 VALU instead of 58) the register budget is what limits kTR: 96 tokens spilled 48 VGPRs to
 // scratch, 80 spill 11 (decode at 10 GB: 96 → 47.7 ms, 80 → 45.9; 72: 47.5, its phase C re-decodes more tails).
+#ifndef SBAM_CHK_SLACK  // (0 reproduces the round-3 gate: tests/test_inflate_streams.py::test_inflate_round_boundary_distance)
+#define SBAM_CHK_SLACK 258
+#endif
 #ifndef SBAM_TR
 #define SBAM_TR 80
 #endif
@@ -1292,7 +1295,9 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         // when this minus the token is below -o0)
         uint32_t bq = 0x7fffu - pl;
         bool first = nst == 0;  // no stop yet
-        const bool chk = out < 32768;  // o0 >= out, and a distance is at most 32768
+        // o0 >= out and a distance is at most 32768, but a lane (or round) that starts in the distance state has
+        // its match begin pl <= 258 bytes before o0: from out >= 32768 + 258 on no distance reaches past the start
+        const bool chk = out < 32768 + SBAM_CHK_SLACK;
         // one symbol, predicated: a lane that is done (stopped out of the data, or past its segment) decodes the
         // same symbol again and commits nothing, so the steps need no exec-mask branches
         // ST: the step's index when it is below kTR (its token goes to tr), else -1

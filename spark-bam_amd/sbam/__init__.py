@@ -122,7 +122,7 @@ RECORD_COLUMNS = {"offset": np.int64, "block_pos": np.int64, "block_off": np.int
 
 
 EXPORTS = [  # every symbol include/sbam.h declares
-    "sbam_open", "sbam_close", "sbam_load", "sbam_last_error", "sbam_set_path", "sbam_reset", "sbam_version", "sbam_find_block_starts", "sbam_scan_blocks",
+    "sbam_open", "sbam_close", "sbam_load", "sbam_reserve", "sbam_last_error", "sbam_set_path", "sbam_reset", "sbam_version", "sbam_find_block_starts", "sbam_scan_blocks",
     "sbam_get_blocks", "sbam_inflate", "sbam_inflate_fallbacks", "sbam_read_uncompressed", "sbam_pos_to_offset", "sbam_offset_to_pos",
     "sbam_header", "sbam_set_contig_lengths", "sbam_check_eager", "sbam_check_full_words", "sbam_check_full_counts",
     "sbam_find_record_start", "sbam_file_splits", "sbam_split_records", "sbam_compute_splits",
@@ -181,6 +181,7 @@ def load_library(path: str = LIB_PATH):
         "sbam_compute_splits": (ctypes.c_int, [vp, P(_SplitArgs), vp, i64, P(i64)]),
         "sbam_record_offsets": (ctypes.c_int, [vp, i64, i64, vp, i64, P(i64)]),
         "sbam_load": (ctypes.c_int, [vp, vp, i64, i64, i64]),
+        "sbam_reserve": (ctypes.c_int, [vp, i64, i64, i64, i64]),
         "sbam_record_spans": (ctypes.c_int, [vp, vp, i64, vp, vp, vp]),
         "sbam_load_records": (ctypes.c_int, [vp, P(_SplitArgs), i64, i64, vp, P(i64)]),
         "sbam_get_record_columns": (ctypes.c_int, [vp, i64, i64, P(_RecordColumns)]),
@@ -334,6 +335,10 @@ class BamFile:
             self.n_ref = self.contig_lengths = self.header_end = None
         self.n_blocks = None
         self.uncompressed_size = None
+
+    def reserve(self, comp_bytes: int, n_blocks: int, ubytes: int, n_records: int = 0):
+        """sbam_reserve: size the device buffers for windows up to these sizes, so no later load reallocates."""
+        self._check(self.L.sbam_reserve(self.ctx, int(comp_bytes), int(n_blocks), int(ubytes), int(n_records)))
 
     @property
     def loads_to_eof(self) -> bool:

@@ -11,6 +11,7 @@ later `apply` in those blocks is a bit (or word) lookup — the shape of the ref
 (HALO: long records) doubles and retries.  INTEGRATION.md shows the same class on the JVM (Panama)."""
 from __future__ import annotations
 
+from collections import OrderedDict
 from typing import Callable, Dict, Optional, Sequence
 
 import numpy as np
@@ -20,45 +21,63 @@ import sbam
 
 class LazyBlockChecker:
     """eager.Checker (`kind="eager"`: apply → bool, eager/Checker.scala:24-126) or full.Checker (`kind="full"`: apply →
-    the sbam.h result word, full/Checker.scala:22-184), computed a window of blocks at a time on first use."""
+    the sbam.h result word, full/Checker.scala:22-184), computed a window of blocks at a time on first use.
+
+    One device context serves every window (opened on the first miss, refilled by sbam_load afterwards: no stream
+    creation, allocation or free per window), and only the calls of the last `keep` windows stay cached: a
+    partition's positions arrive in file order (PosIterator over its blocks), so older windows are not asked again —
+    and a revisited one is simply recomputed."""
 
     def __init__(self, source: Callable[[int, int], np.ndarray], file_size: int, contig_lengths: Sequence[int],
                  reads_to_check: int = sbam.READS_TO_CHECK, window: int = 4 << 20, device: int = 0,
-                 kind: str = "eager"):
-        assert kind in ("eager", "full")
+                 kind: str = "eager", keep: int = 2):
+        assert kind in ("eager", "full") and keep >= 1
         self.source, self.file_size = source, int(file_size)
         self.contig_lengths = np.asarray(contig_lengths, np.int64)
-        self.R, self.window, self.device, self.kind = reads_to_check, int(window), device, kind
-        self.cache: Dict[int, np.ndarray] = {}  # block start → calls at offsets 0 .. usize-1
+        self.R, self.window, self.device, self.kind, self.keep = reads_to_check, int(window), device, kind, keep
+        self.windows: "OrderedDict[int, Dict[int, np.ndarray]]" = OrderedDict()  # window start → {block start → calls}
+        self.cache: Dict[int, np.ndarray] = {}  # block start → calls at offsets 0 .. usize-1 (the kept windows)
         self.bulk_calls = 0                      # GPU windows computed (one per cache miss, plus HALO retries)
+        self.f: Optional[sbam.BamFile] = None
+
+    def _load(self, lo: int, hi: int):
+        data = self.source(lo, hi)
+        if self.f is None:
+            self.f = sbam.BamFile(data, device=self.device, base_offset=lo, file_size=self.file_size, inflate=False)
+        else:
+            self.f.load(data, base_offset=lo, file_size=self.file_size)
+        return self.f
 
     def _fill(self, block_pos: int):
         win = self.window
         while True:
             lo, hi = block_pos, min(self.file_size, block_pos + win)
             self.bulk_calls += 1
-            with sbam.BamFile(self.source(lo, hi), device=self.device, base_offset=lo, file_size=self.file_size,
-                              inflate=False) as f:
-                f.run(contig_lengths=self.contig_lengths)
-                st, cs, us, uo = f.blocks()
-                if st.size == 0 or int(st[0]) != block_pos:
-                    raise sbam.SbamError(f"no BGZF block starts at {block_pos}")
-                # the blocks of the first half of the window (all of them when it reaches EOF): the second half is the
-                # halo their chains read
-                end = hi if f.loads_to_eof else lo + (hi - lo) // 2
-                nb = max(1, int(np.searchsorted(st + cs, end, side="right")))
-                x1 = int(uo[nb - 1]) + int(us[nb - 1])
-                try:
-                    calls = (f.check_eager(0, x1, self.R) if self.kind == "eager" else
-                             f.check_full_words(0, x1, self.R))
-                except sbam.HaloException:
-                    if hi >= self.file_size:
-                        raise
-                    win *= 2
-                    continue
-                for b in range(nb):
-                    self.cache[int(st[b])] = calls[int(uo[b]): int(uo[b]) + int(us[b])].copy()
-                return
+            f = self._load(lo, hi)
+            f.run(contig_lengths=self.contig_lengths)
+            st, cs, us, uo = f.blocks()
+            if st.size == 0 or int(st[0]) != block_pos:
+                raise sbam.SbamError(f"no BGZF block starts at {block_pos}")
+            # the blocks of the first half of the window (all of them when it reaches EOF): the second half is the
+            # halo their chains read
+            end = hi if f.loads_to_eof else lo + (hi - lo) // 2
+            nb = max(1, int(np.searchsorted(st + cs, end, side="right")))
+            x1 = int(uo[nb - 1]) + int(us[nb - 1])
+            try:
+                calls = (f.check_eager(0, x1, self.R) if self.kind == "eager" else
+                         f.check_full_words(0, x1, self.R))
+            except sbam.HaloException:
+                if hi >= self.file_size:
+                    raise
+                win *= 2
+                continue
+            blocks = {int(st[b]): calls[int(uo[b]): int(uo[b]) + int(us[b])] for b in range(nb)}
+            self.windows[lo] = blocks
+            while len(self.windows) > self.keep:
+                for k in self.windows.popitem(last=False)[1]:
+                    self.cache.pop(k, None)
+            self.cache.update(blocks)
+            return
 
     def apply(self, pos: sbam.Pos):
         calls = self.cache.get(pos.block_pos)
@@ -69,6 +88,18 @@ class LazyBlockChecker:
         return bool(v) if self.kind == "eager" else int(v)
 
     __call__ = apply
+
+    def close(self):
+        """The partition is done (CallPartition's .finish(close)): release the device context."""
+        if self.f is not None:
+            self.f.close()
+            self.f = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
 
 
 def make_checker(contig_lengths: Sequence[int], reads_to_check: int = sbam.READS_TO_CHECK, kind: str = "eager",

@@ -668,14 +668,18 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
             else:
                 sys.stdout.write(text)
         return 0
+    dev = getattr(a, "device", None) or 0
     if a.cmd == "full-check" and a.windows == 0:
         from sbam import dist as sdist
         src, size = sdist.file_source(a.bam)
-        a.windows = sdist.auto_windows(size, src, sdist.device_free_bytes(0), contexts=1)
+        # the budget leaves room for halo retries: a window's halo can grow 4x per HaloException (2 -> 8 -> 32 MiB
+        # of compressed bytes and beyond), each compressed byte costing hbm_bytes_per_compressed_byte in HBM
+        margin = int(sdist.hbm_bytes_per_compressed_byte(3.3) * (128 << 20))
+        a.windows = sdist.auto_windows(size, src, max(1, sdist.device_free_bytes(dev) - margin), contexts=1)
     if a.cmd == "full-check" and a.windows > 1:
         from sbam import dist as sdist
         parts = sdist.full_check_file(a.bam, a.print_limit, a.intervals, a.reads_to_check, world=a.windows,
-                                      device=0, records_path=a.bam + ".records")
+                                      device=dev, records_path=a.bam + ".records")
         text = "\n".join(full_check_lines(parts, a.print_limit)) + "\n"
         if a.out:
             open(a.out, "w").write(text)
@@ -683,7 +687,7 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
             sys.stdout.write(text)
         return 0
     data = open(a.bam, "rb").read()
-    with sbam.BamFile(data, path=a.bam) as f:
+    with sbam.BamFile(data, path=a.bam, device=dev) as f:
         if a.cmd == "full-check":
             rep = FullCheckReport(f, data, a.bam + ".records", a.print_limit, a.intervals, a.reads_to_check)
             lines = rep.lines()

@@ -146,6 +146,7 @@ class GpuShard:
             self.f.close()
         self.f = self.sbam.BamFile(self.source(lo, hi), device=self.device, base_offset=lo,
                                    file_size=self.plan.file_size, inflate=False)
+        self._reserved = 0  # a new context (WindowPipe._reserve sizes it again)
 
     def reload(self, plan: ShardPlan, data: np.ndarray, source: Optional[Callable[[int, int], np.ndarray]] = None):
         """Stream the next byte-range window through this shard's context (sbam_load: device allocations are
@@ -286,6 +287,28 @@ def bgzf_ratio(source: Callable[..., np.ndarray], size: int, sample: int = 8 << 
         comp += bsize + 1
         pos = end
     return unc / comp if comp and unc else 3.0
+
+
+def bgzf_buffer_stats(buf: np.ndarray) -> Tuple[float, float]:
+    """(uncompressed / compressed, compressed bytes per block) over the BGZF block chain from the first header in
+    `buf` (as bgzf_ratio); (3.0, 65536.0) when nothing parses."""
+    raw = buf[: 8 << 20].tobytes()
+    pos = 0
+    while True:
+        pos = raw.find(b"\x1f\x8b\x08\x04", pos)
+        if pos < 0 or raw[pos + 12:pos + 14] == b"BC":
+            break
+        pos += 1
+    comp = unc = nb = 0
+    while pos >= 0 and pos + 18 <= len(raw) and raw[pos] == 0x1F and raw[pos + 1] == 0x8B:
+        end = pos + (raw[pos + 16] | (raw[pos + 17] << 8)) + 1
+        if end > len(raw):
+            break
+        unc += int.from_bytes(raw[end - 4:end], "little")
+        comp += end - pos
+        nb += 1
+        pos = end
+    return (unc / comp, comp / nb) if comp and unc else (3.0, 65536.0)
 
 
 def auto_windows(size: int, source: Callable[..., np.ndarray], free_bytes: int, contexts: int = 2,
@@ -539,6 +562,7 @@ class WindowPipe:
         self.loader = ThreadPoolExecutor(max_workers=1)
         self.stager = ThreadPoolExecutor(max_workers=1)
         self.ctx = [None, None]
+        self._inflight = []   # loader futures of the running step
         self.g = 0            # global number of the next step's window 0
         self._next = None     # (load future of window g, {g': staged future}) carried over from the last step
 
@@ -562,7 +586,20 @@ class WindowPipe:
             self.ctx[j] = GpuShard(wp, src, self.split_size, self.contig_lengths, device=self.device, halo=self.halo)
         else:
             self.ctx[j].reload(wp, buf, src)
+        self._reserve(self.ctx[j], buf)
         return self.ctx[j]
+
+    def _reserve(self, sh, buf):
+        """Size a context once for the largest window of the plan (device buffers are grow-only: a context that
+        first meets a larger window than before would hipFree + hipMalloc tens of GB inside a timed step), from the
+        compression ratio and block size of the staged bytes (+12 %)."""
+        comp = max(p.load_range(sh.halo)[1] - p.load_range(sh.halo)[0] for p in self.wplans)
+        if getattr(sh, "_reserved", 0) >= comp:
+            return
+        ratio, per_block = bgzf_buffer_stats(buf)
+        U = int(comp * ratio * 1.12) + (1 << 20)
+        sh.f.reserve(comp, int(comp / per_block * 1.12) + 1024, U, U // 200)
+        sh._reserved = comp
 
     def _source(self, lo, hi, buf):
         """The byte source of one loaded window: its staged bytes for its own range; any other range (a halo retry)
@@ -583,13 +620,28 @@ class WindowPipe:
     def step(self) -> list:
         W = len(self.wplans)
         g0 = self.g
-        out = []
         if self._next is not None:
             fut, staged = self._next
             self._next = None
         else:
             staged = {g: self.stager.submit(self._stage, g) for g in range(g0, g0 + min(2, W))}
             fut = None
+        try:
+            return self._windows(g0, W, staged, fut)
+        except BaseException:
+            # a failed window (a non-halo error, or a halo retry that reached EOF): drain the loads and stagings still
+            # in flight — they drive the other context and the staging buffers — so that a retried step starts clean
+            for f in ([fut] if fut is not None else []) + list(staged.values()) + list(self._inflight):
+                try:
+                    f.result()
+                except BaseException:
+                    pass
+            self._inflight = []
+            self._next = None
+            raise
+
+    def _windows(self, g0, W, staged, fut) -> list:
+        self._inflight = []
         sh = self._load(g0, staged[g0]) if fut is None else None
         dbg = os.environ.get("SBAM_PIPE_DEBUG")
         for w in range(W):
@@ -604,6 +656,7 @@ class WindowPipe:
                 if g + 1 not in staged:
                     staged[g + 1] = self.stager.submit(self._stage, g + 1)
                 fut = self.loader.submit(self._load, g + 1, staged[g + 1])
+                self._inflight.append(fut)
             if (w + 2 < W or self.prefetch) and g + 2 not in staged:
                 staged[g + 2] = self.stager.submit(self._stage, g + 2)
             t1 = time.perf_counter()

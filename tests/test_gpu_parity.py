@@ -238,3 +238,36 @@ def test_lazy_block_checker_drop_in(tmp_path, name, window, kind):
         got = [chk(sbam.Pos(int(st[b]), int(o))) for o in offs]
         assert got == [bool(want[uo[b] + o]) if kind == "eager" else int(want[uo[b] + o]) for o in offs], b
     assert 1 < chk.bulk_calls < st.size
+
+
+@pytest.mark.gpu
+def test_lazy_block_checker_windows_timed(tmp_path):
+    """100+ lazy 4 MB windows through ONE kept context (sbam_load per window, no per-window context setup): the calls
+    at sampled offsets of every block equal a resident whole-file check, only the last `keep` windows stay cached,
+    and the ms per bulk call is printed (CallPartition.scala:35-53 calls Checker.apply per position of each block)."""
+    import time
+    import sbam
+    import synth
+    from sbam import dist as sdist
+    from sbam.checker import LazyBlockChecker
+    s = synth.SynthBam(tile_mb=220)
+    path = tmp_path / "synth.bam"
+    path.write_bytes(s.bytes().tobytes())
+    with sbam.BamFile(s.bytes()) as f:
+        want = f.check_eager()
+        st, cs, us, uo = f.blocks()
+    chk = LazyBlockChecker(*sdist.file_source(str(path)), s.contig_lengths, window=4 << 20)
+    rng = np.random.default_rng(3)
+    t0 = time.perf_counter()
+    bad = 0
+    for b in range(st.size):
+        offs = rng.integers(0, int(us[b]), 16)
+        got = np.array([chk(sbam.Pos(int(st[b]), int(o))) for o in offs])
+        bad += int((got != want[uo[b] + offs].astype(bool)).sum())
+        assert len(chk.windows) <= 2
+    dt = time.perf_counter() - t0
+    chk.close()
+    assert bad == 0
+    assert chk.bulk_calls >= 100
+    print(f"lazy checker: {chk.bulk_calls} windows of 4 MB, {1e3 * dt / chk.bulk_calls:.2f} ms per bulk call "
+          f"(incl. the host preads and lookups)")

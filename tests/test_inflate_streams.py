@@ -158,3 +158,94 @@ def test_scan_many_small_blocks(n_blocks):
         assert np.array_equal(starts, want)
     finally:
         g.close()
+
+
+# ---- a hand-placed fixed-Huffman stream: a round boundary of the wave decoder between a length and its distance --
+class _BitWriter:
+    def __init__(self):
+        self.bits = []
+
+    def put(self, v: int, n: int):  # n bits of v, LSB first (header fields, extra bits)
+        self.bits += [(v >> i) & 1 for i in range(n)]
+
+    def code(self, c: int, n: int):  # a Huffman code, MSB first
+        self.bits += [(c >> (n - 1 - i)) & 1 for i in range(n)]
+
+    def lit(self, b: int):
+        assert b < 144
+        self.code(0x30 + b, 8)
+
+    def len258(self):
+        self.code(0xC0 + 5, 8)  # symbol 285, no extra bits
+
+    def dist(self, d: int):
+        if d == 1:
+            self.code(0, 5)
+        else:
+            assert d == 32768
+            self.code(29, 5)
+            self.put(d - 24577, 13)
+
+    def tobytes(self) -> bytes:
+        b = self.bits + [0] * (-len(self.bits) % 8)
+        return bytes(sum(b[i + j] << j for j in range(8)) for i in range(0, len(b), 8))
+
+
+def straddle_stream(distance_ok: bool):
+    """One final fixed-Huffman block whose first 64 x 544-bit round ends inside a 258-byte length symbol, with
+    32768 <= bytes out (including that match) < 32768 + 258; its distance (the next round's first symbol, decoded
+    in the distance state with the pending length) reaches exactly back to the block start (valid) or one byte
+    further (zlib: "invalid distance too far back").  The wave decoder's "no distance can reach past the start"
+    shortcut must still check it (the round starts in the distance state)."""
+    B = 3 + 64 * 544  # bit of the first round's end, from the payload start
+    for n_m in range(100, 128):
+        for n9 in range(0, 8):  # 9-bit literals (144..255) shift the bit count by one each
+            rest = B - 8 - 11 - 13 * n_m - 9 * n9
+            if rest < 0:
+                continue
+            n8 = rest // 8 + (1 if rest % 8 else 0)  # pos_c in [B - 8, B - 1]
+            pos_c = 11 + 13 * n_m + 9 * n9 + 8 * n8
+            out_after = 1 + 258 * n_m + n9 + n8 + 258
+            if B - 8 <= pos_c < B and 32768 <= out_after < 32768 + 258 and out_after - 258 < 32768:
+                w = _BitWriter()
+                w.put(1, 1)
+                w.put(1, 2)
+                w.lit(65)
+                for _ in range(n_m):
+                    w.len258()
+                    w.dist(1)
+                for i in range(n9):
+                    w.code(0x190 + (i % 100), 9)  # literal 144 + i
+                for i in range(n8):
+                    w.lit(33 + i % 90)
+                assert len(w.bits) == pos_c
+                w.len258()
+                start = out_after - 258
+                if distance_ok:
+                    # the furthest valid distance from this match start: back to byte 0 (d = start <= 32767)
+                    w.code(29 if start > 24576 else 28, 5)
+                    w.put(start - (24577 if start > 24576 else 16385), 13 if start > 24576 else 13)
+                else:
+                    w.dist(32768)  # 32768 > start: too far back
+                w.code(0, 7)  # end of block
+                return w.tobytes(), out_after
+    raise AssertionError("no layout")
+
+
+def straddle_file(distance_ok: bool) -> bytes:
+    payload, n = straddle_stream(distance_ok)
+    return bgzf_block(payload, n) + EOF_BLOCK
+
+
+def test_oracle_straddle_distance():
+    kind, out = oracle_result(straddle_file(True))
+    assert kind == "ok" and len(out) == straddle_stream(True)[1]
+    kind, msg = oracle_result(straddle_file(False))
+    assert kind == "error" and msg.startswith("Expected %d decompressed bytes" % straddle_stream(False)[1]), msg
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("distance_ok", [True, False])
+def test_inflate_round_boundary_distance(distance_ok):
+    data = straddle_file(distance_ok)
+    assert gpu_result(data) == oracle_result(data)
