@@ -80,7 +80,8 @@ def measured_traffic(kernel: str, args):
             t = json.load(open(path))
         except (OSError, ValueError):
             continue
-        if t.get("workload") != {"size_gb": args.size_gb, "seed": args.seed, "tile_mb": args.tile_mb}:
+        if t.get("workload") != {"size_gb": args.size_gb, "seed": args.seed, "tile_mb": args.tile_mb,
+                                 "tiles": args.tiles}:
             continue
         if t.get("source_digest") != digest:
             continue
@@ -91,36 +92,34 @@ def measured_traffic(kernel: str, args):
 
 
 def copy_peak(dev) -> dict:
-    """Measured HBM copy rate on this GPU: a 4 GiB device-to-device tensor copy (read + write bytes / time)."""
-    import torch
+    """Measured HBM copy peak on this GPU: tools/hbm_peak.hip (16-B nontemporal loads/stores, 4 in flight per lane,
+    grid-stride) over 4 GiB device to device, read + write bytes / kernel time; the best of a few grid sizes."""
+    import ctypes
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "build", "libhbmpeak.so"))
+    lib.hbm_copy_peak.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                  ctypes.POINTER(ctypes.c_double)]
     n = 4 << 30
-    a = torch.empty(n // 8, dtype=torch.int64, device=dev)
-    b = torch.empty_like(a)
-    a.fill_(1)
-    for _ in range(2):
-        b.copy_(a)
-    torch.cuda.synchronize(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = 10
-    e0.record()
-    for _ in range(reps):
-        b.copy_(a)
-    e1.record()
-    torch.cuda.synchronize(dev)
-    ms = e0.elapsed_time(e1) / reps
-    del a, b
-    torch.cuda.empty_cache()
-    return {"value": round(2 * n / (ms * 1e-3) / 1e9, 1), "unit": "GB/s", "bytes": 2 * n,
-            "how": "torch int64 copy_ of 4 GiB device->device, read+write bytes / time, 10 reps"}
+    best = None
+    for grid in (1024, 2048, 4096, 8192):
+        ms = ctypes.c_double(0.0)
+        rc = lib.hbm_copy_peak(dev.index or 0, n, 10, grid, ctypes.byref(ms))
+        if rc == 0 and ms.value > 0 and (best is None or ms.value < best[1]):
+            best = (grid, ms.value)
+    if best is None:
+        raise RuntimeError("hbm_copy_peak failed")
+    return {"value": round(2 * n / (best[1] * 1e-3) / 1e9, 1), "unit": "GB/s", "bytes": 2 * n,
+            "how": f"tools/hbm_peak.hip: global_load/store_dwordx4 (nontemporal) copy of 4 GiB device->device, "
+                   f"read+write bytes / kernel time, 10 reps, best grid {best[0]} x 256"}
 
 
-def cpu_baseline(sample_mb: float, threads: int, split_size: int, seed: int):
+def cpu_baseline(sample_mb: float, threads: int, split_size: int, seed: int, tiles: int = 1):
     """Oracle (C restatement of the reference algorithm) on a bounded sample of the same synthetic stream:
     zlib inflate + full checker at every position + compute-splits, `threads` host threads."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     import synth
-    s = synth.SynthBam.for_size(int(sample_mb * 1e6), tile_mb=min(64.0, sample_mb), seed=seed, threads=threads)
+    s = synth.SynthBam.for_size(int(sample_mb * 1e6), tile_mb=min(64.0, sample_mb), seed=seed, threads=threads,
+                                distinct=tiles > 1, cycle=max(tiles, 1))
     data = s.bytes()
     t0 = time.perf_counter()
     f = oracle.BamFile(data, threads=threads)
@@ -134,14 +133,15 @@ def cpu_baseline(sample_mb: float, threads: int, split_size: int, seed: int):
                       f"compute-splits @ {split_size >> 20} MiB, {wall:.2f} s wall"}
 
 
-def cpu_baseline_load_reads(sample_mb: float, threads: int, split_size: int, seed: int):
+def cpu_baseline_load_reads(sample_mb: float, threads: int, split_size: int, seed: int, tiles: int = 1):
     """Oracle on a bounded sample for the loadReads workload (configs[3]): zlib inflate (`threads` host threads)
     then, per Hadoop split, FindBlockStart → FindRecordStart → the record chain (CanLoadBam.scala:281-334).  The
     oracle stops at record offsets (no field decode into columns), so the CPU side does less work than the GPU."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     import synth
-    s = synth.SynthBam.for_size(int(sample_mb * 1e6), tile_mb=min(64.0, sample_mb), seed=seed, threads=threads)
+    s = synth.SynthBam.for_size(int(sample_mb * 1e6), tile_mb=min(64.0, sample_mb), seed=seed, threads=threads,
+                                distinct=tiles > 1, cycle=max(tiles, 1))
     data = s.bytes()
     t0 = time.perf_counter()
     f = oracle.BamFile(data, threads=threads)
@@ -163,6 +163,8 @@ def main():
     ap.add_argument("--size-gb", type=float, default=10.0, help="compressed GB per GPU")
     ap.add_argument("--split-mb", type=float, default=2.0)
     ap.add_argument("--tile-mb", type=float, default=64.0)
+    ap.add_argument("--tiles", type=int, default=16,
+                    help="distinct seeded tiles the synthetic file cycles through (1: one tile repeated)")
     ap.add_argument("--threads", type=int, default=0, help="host threads (generator, CPU baseline); 0 = the host share")
     ap.add_argument("--cpu-sample-mb", type=float, default=2000.0,
                     help="compressed MB of the same synthetic file timed on the CPU oracle (~10 s at 16 threads)")
@@ -215,7 +217,9 @@ def main():
     split_size = int(args.split_mb * (1 << 20))
     t = time.time()
     s = synth.SynthBam.for_size(int(args.size_gb * 1e9 * world), tile_mb=args.tile_mb, seed=args.seed,
-                                threads=threads, read_len=args.read_len)
+                                threads=threads, read_len=args.read_len, distinct=args.tiles > 1,
+                                cycle=max(args.tiles, 1))
+    setup_s = time.time() - t
     plans = sdist.plan_shards(s.size, split_size, world)  # rank-level plans (what all_gather sees)
     plan = plans[rank]
     W = args.windows
@@ -401,7 +405,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline and args.read_len == 150:
             try:
                 base_fn = cpu_baseline if args.workload == "full-check" else cpu_baseline_load_reads
-                cpu = base_fn(args.cpu_sample_mb, threads, split_size, args.seed)
+                cpu = base_fn(args.cpu_sample_mb, threads, split_size, args.seed, args.tiles)
                 cpu["host_nproc"] = nproc
             except Exception as e:  # reported, never substituted for the GPU number
                 log(f"cpu baseline failed: {e!r}")
@@ -425,9 +429,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (tools/synth_bam.c: %s, zlib-6 BGZF, seed %#x)" % (
+            "data": "synthetic (tools/synth_bam.c: %s, zlib-6 BGZF, seed %#x, %s)" % (
                 "150bp paired Illumina-like" if args.read_len == 150 else "long-read 10-50 kb" if args.read_len == 0
-                else f"{args.read_len} bp", args.seed),
+                else f"{args.read_len} bp", args.seed,
+                f"a cycle of {min(args.tiles, s.copies)} distinct {args.tile_mb:g} MB tiles" if args.tiles > 1
+                else f"one {args.tile_mb:g} MB tile repeated"),
             "config": {"workload": ("Synthetic %.0f GB %s BAM per GPU: " % (
                                    args.size_gb, "Illumina-like" if args.read_len == 150 else
                                    "long-read" if args.read_len == 0 else f"{args.read_len} bp")) +
@@ -436,7 +442,8 @@ def main():
                                     % args.split_mb),
                        "file_gb": round(s.size / 1e9, 3), "uncompressed_gb_per_gpu": round(U / 1e9, 3),
                        "records": s.n_records, "blocks_per_gpu": nblocks, "split_mb": args.split_mb,
-                       "windows_per_gpu": W, "parallelism": f"shard{world}"},
+                       "windows_per_gpu": W, "parallelism": f"shard{world}",
+                       "tiles": min(args.tiles, s.copies), "setup_s": round(setup_s, 1)},
             "uncompressed_gbps": round(U * world * args.steps / elapsed / 1e9, 3),
             "kernel_ms": {k: round(v, 3) for k, v in avg.items()},
             "roofline": {"bound": "hbm", "kernel": names[dom], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,

@@ -66,6 +66,7 @@ struct sbam_ctx {
   size_t bitmap_cap = 0;
   int64_t bm_x0 = 0, bm_x1 = 0;
   bool bm_valid = false;
+  bool bm_list = false;  // the bitmap came from the list-form chain pass: d_nfb[1..2] describe its links
   int32_t bm_R = -1;
   // inflate scratch: token pages of the decode → resolve path
   uint8_t *d_pool = nullptr;  // token regions (inflate_token_bytes)
@@ -778,6 +779,7 @@ int sbam_check_full_words(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, uint32
     Timer t(c, "check_words");
     HIPCHK(c, launch_check_words(view(c), x0, x1, R, d_w, c->d_bitmap, c->stream));
   }
+  c->bm_list = false;
   c->bm_x0 = x0 & ~(int64_t)63;
   c->bm_x1 = x1;
   c->bm_R = R;
@@ -801,16 +803,18 @@ static hipError_t run_chains(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, int
   int64_t total = 0;
   if ((e = hipMemcpyAsync(&total, c->d_coff2 + nch, 8, hipMemcpyDeviceToHost, c->stream)) != hipSuccess) return e;
   if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return e;
+  c->bm_list = false;
   if (total > cap) return launch_check_full_chains(view(c), x0, x1, R, by_key, cd, c->d_bitmap, c->stream);
   const size_t n = (size_t)std::max<int64_t>(total, 1);
   if ((e = ensure(&c->d_plist, &c->plist_cap, n)) != hipSuccess) return e;
   if ((e = ensure(&c->d_pfb, &c->pfb_cap, n)) != hipSuccess) return e;
   if ((e = ensure(&c->d_pok, &c->pok_cap, n)) != hipSuccess) return e;
-  if ((e = ensure(&c->d_nfb, &c->nfb_cap, 1)) != hipSuccess) return e;
+  if ((e = ensure(&c->d_nfb, &c->nfb_cap, 3)) != hipSuccess) return e;
   cs.list = c->d_plist;
   cs.ok = c->d_pok;
   cs.fb = c->d_pfb;
   cs.n_fb = c->d_nfb;
+  c->bm_list = true;
   return launch_chain_list_run(view(c), x0, x1, R, by_key, cd, c->d_bitmap, cs, c->stream);
 }
 
@@ -989,7 +993,8 @@ static int split_counts(sbam_ctx *c, bool try_bitmap, const std::vector<int64_t>
     int32_t *d_fail = reinterpret_cast<int32_t *>(c->d_small + 8);
     const int64_t xa = c->bm_x0 & ~(int64_t)63;
     HIPCHK(c, hipMemsetAsync(d_fail, 0, 4, c->stream));
-    HIPCHK(c, launch_chain_proof(c->d_u, c->L, c->d_bitmap, xa, X0, X1, d_fail, c->stream));
+    HIPCHK(c, launch_chain_proof(c->d_u, c->L, c->d_bitmap, xa, X0, X1, d_fail, c->bm_list ? c->d_nfb : nullptr,
+                                 c->stream));
     HIPCHK(c, launch_split_popcounts(c->d_bitmap, xa, c->d_sx, c->d_se, n, c->d_sn, d_fail, c->stream));
     int32_t fail = 1;
     HIPCHK(c, hipMemcpyAsync(&fail, d_fail, 4, hipMemcpyDeviceToHost, c->stream));

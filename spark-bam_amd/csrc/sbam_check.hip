@@ -433,17 +433,25 @@ __global__ __launch_bounds__(256) void k_p0_links(StreamView sv, const int64_t *
   }
 }
 
-// Success when the R-1 links from p_i hold; every other PASS0 position goes to the fallback list.
+// Success when the R-1 links from p_i hold; every other PASS0 position goes to the fallback list.  n_fb[1] counts
+// the missing links between consecutive list entries: with none (and no failing fallback, n_fb[2]) the success
+// bitmap IS the list and every set bit hops to the next one — the chain proof of the split records
+// (sbam_records.hip) then holds without another pass over the records.
 __global__ __launch_bounds__(256) void k_p0_fast(const int64_t *__restrict__ list, const int64_t *__restrict__ n_ptr,
                                                  const uint8_t *__restrict__ ok, int R, CountsDev cd,
                                                  int64_t *__restrict__ fb, unsigned long long *__restrict__ n_fb) {
   const int64_t n = *n_ptr;
-  uint32_t n_succ = 0;
+  uint32_t n_succ = 0, n_gap = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     bool succ = i + (R - 1) <= n - 1 || R <= 1;
     for (int k = 0; succ && k < R - 1; k++) succ = ok[i + k] != 0;
     if (succ) n_succ++;
     else fb[atomicAdd(n_fb, 1ull)] = list[i];
+    n_gap += (i + 1 < n && !ok[i]) ? 1u : 0u;
+  }
+  if (__ballot(n_gap != 0)) {
+    n_gap = wave_sum(n_gap);
+    if (lane_id() == 0) atomicAdd(&n_fb[1], (unsigned long long)n_gap);
   }
   if (cd.counts) {
     n_succ = wave_sum(n_succ);
@@ -454,14 +462,18 @@ __global__ __launch_bounds__(256) void k_p0_fast(const int64_t *__restrict__ lis
 __global__ __launch_bounds__(256) void k_p0_fallback(StreamView sv, int64_t x0a, int64_t x1, int R,
                                                      unsigned long long *__restrict__ bitmap, CountsDev cd, int bykey,
                                                      const int64_t *__restrict__ fb,
-                                                     const unsigned long long *__restrict__ n_fb) {
+                                                     unsigned long long *__restrict__ n_fb) {
   const int64_t n = (int64_t)*n_fb;
   uint32_t n_succ = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t p = fb[i];
     const uint32_t w = walk_chain(sv, bitmap, x0a, x1, p, R);
-    if (w & W_SUCC) n_succ++;
-    else atomicAnd(&bitmap[(p - x0a) >> 6], ~(1ull << ((p - x0a) & 63)));
+    if (w & W_SUCC) {
+      n_succ++;
+    } else {
+      atomicAnd(&bitmap[(p - x0a) >> 6], ~(1ull << ((p - x0a) & 63)));
+      atomicAdd(&n_fb[2], 1ull);
+    }
     if (cd.counts) count_chain_result(cd, w, bykey != 0);
   }
   if (cd.counts) {
@@ -1645,7 +1657,7 @@ hipError_t launch_chain_list_run(StreamView sv, int64_t x0, int64_t x1, int32_t 
   const int64_t *n_ptr = cs.chunk_off + nch;
   hipLaunchKernelGGL(k_p0_list, dim3((unsigned)nch), dim3(256), 0, s, bitmap, nwords, x0a, cs.chunk_off, cs.list);
   hipLaunchKernelGGL(k_p0_links, dim3(4096), dim3(256), 0, s, sv, cs.list, n_ptr, cs.ok);
-  (void)hipMemsetAsync(cs.n_fb, 0, sizeof(unsigned long long), s);
+  (void)hipMemsetAsync(cs.n_fb, 0, 3 * sizeof(unsigned long long), s);  // fallbacks, missing links, failed fallbacks
   hipLaunchKernelGGL(k_p0_fast, dim3(4096), dim3(256), 0, s, cs.list, n_ptr, cs.ok, (int)R, cd, cs.fb, cs.n_fb);
   hipLaunchKernelGGL(k_p0_fallback, dim3(1024), dim3(256), 0, s, sv, x0a, x1, (int)R, bitmap, cd, (int)by_key, cs.fb,
                      cs.n_fb);

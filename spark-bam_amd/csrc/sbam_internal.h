@@ -77,7 +77,8 @@ hipError_t launch_gather_blocks(const Candidate *cands, int64_t first, int64_t n
 // exact path for the blocks it hands over), then LZ77 resolve into `out`.  tok: inflate_token_bytes(L, nb) bytes;
 // slow: nb int32; counters: 3 × u32 device scratch, reset by the decode launch.
 inline size_t inflate_token_bytes(int64_t L, int64_t nb) {
-  return ((2 * (size_t)L + 15) & ~(size_t)15) + 32 * (size_t)nb + 256;
+  // (+1 KiB: the resolver reads up to 4 x 64 + 1 tokens past a step's start)
+  return ((2 * (size_t)L + 15) & ~(size_t)15) + 32 * (size_t)nb + 1024;
 }
 hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *tok, int32_t *status,
                                  int32_t *found, int32_t *slow, unsigned int *counters, hipStream_t s);
@@ -120,7 +121,7 @@ hipError_t launch_record_offsets(StreamView sv, int64_t x0, int64_t x_end, int64
 // Record chains of splits and record decode (sbam_records.hip).  Bitmaps as for the checker: bit (x - xa) = call
 // at x, xa 64-aligned.  fail: i32 device flag, set to 1 when the chain is not the bitmap's set bits.
 hipError_t launch_chain_proof(const uint8_t *u, int64_t L, const unsigned long long *bm, int64_t xa, int64_t X0,
-                              int64_t X1, int32_t *fail, hipStream_t s);
+                              int64_t X1, int32_t *fail, const unsigned long long *exact, hipStream_t s);
 hipError_t launch_split_popcounts(const unsigned long long *bm, int64_t xa, const int64_t *xs, const int64_t *xe,
                                   int64_t n, int64_t *counts, int32_t *fail, hipStream_t s);
 hipError_t launch_split_offsets(const unsigned long long *bm, int64_t xa, const int64_t *xs, const int64_t *xe,

@@ -86,8 +86,13 @@ SB_DEV bool hop_ok(const unsigned long long *bm, int64_t xa, int64_t p, int64_t 
 }  // namespace
 
 // One thread per bitmap word of [X0, X1): every set bit p in it must hop to the next set bit (or past X1).
+// exact (may be null): the chain-list counters of the check that left the bitmap ([1] missing links, [2] failed
+// fallback walks, k_p0_fast): both zero means every set bit already hops to the next one (the list pass checked
+// p + 4 + block_size == next PASS0 position for each), so the proof holds without reading the records again.
 __global__ void k_chain_proof(const uint8_t *__restrict__ u, int64_t L, const unsigned long long *__restrict__ bm,
-                              int64_t xa, int64_t X0, int64_t X1, int32_t *__restrict__ fail) {
+                              int64_t xa, int64_t X0, int64_t X1, int32_t *__restrict__ fail,
+                              const unsigned long long *__restrict__ exact) {
+  if (exact && exact[1] == 0 && exact[2] == 0) return;
   const int64_t w0 = (X0 - xa) >> 6, w1 = (X1 - 1 - xa) >> 6;
   for (int64_t w = w0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w <= w1;
        w += (int64_t)gridDim.x * blockDim.x) {
@@ -274,12 +279,12 @@ hipError_t launch_record_spans(const uint8_t *u, int64_t L, const int64_t *offs,
 }
 
 hipError_t launch_chain_proof(const uint8_t *u, int64_t L, const unsigned long long *bm, int64_t xa, int64_t X0,
-                              int64_t X1, int32_t *fail, hipStream_t s) {
+                              int64_t X1, int32_t *fail, const unsigned long long *exact, hipStream_t s) {
   if (X1 <= X0) return hipSuccess;
   const int64_t words = ((X1 - 1 - xa) >> 6) - ((X0 - xa) >> 6) + 1;
   int64_t g = (words + 255) / 256;
   if (g > 16384) g = 16384;
-  hipLaunchKernelGGL(k_chain_proof, dim3((unsigned)g), dim3(256), 0, s, u, L, bm, xa, X0, X1, fail);
+  hipLaunchKernelGGL(k_chain_proof, dim3((unsigned)g), dim3(256), 0, s, u, L, bm, xa, X0, X1, fail, exact);
   return hipGetLastError();
 }
 hipError_t launch_split_popcounts(const unsigned long long *bm, int64_t xa, const int64_t *xs, const int64_t *xe,

@@ -642,6 +642,7 @@ class WindowPipe:
 
     def _windows(self, g0, W, staged, fut) -> list:
         self._inflight = []
+        out = []
         sh = self._load(g0, staged[g0]) if fut is None else None
         dbg = os.environ.get("SBAM_PIPE_DEBUG")
         for w in range(W):

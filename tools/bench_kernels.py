@@ -19,10 +19,12 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--only", default="scan,inflate,check_full,check_eager,splits")
     ap.add_argument("--read-len", type=int, default=150)
+    ap.add_argument("--tiles", type=int, default=16, help="distinct tiles cycled (bench.py's default input)")
     args = ap.parse_args()
     import sbam
     import synth
-    s = synth.SynthBam.for_size(int(args.size_gb * 1e9), tile_mb=min(64.0, args.size_gb * 300), read_len=args.read_len)
+    s = synth.SynthBam.for_size(int(args.size_gb * 1e9), tile_mb=min(64.0, args.size_gb * 300), read_len=args.read_len,
+                                distinct=args.tiles > 1, cycle=max(args.tiles, 1))
     data = s.bytes()
     f = sbam.BamFile(data, inflate=False)
     f.reset()

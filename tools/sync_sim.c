@@ -91,6 +91,8 @@ static int ntrue, tcap;
 static uint8_t *mA[2];  // phase-A symbol starts per state, bit offsets [seg_start, seg_end + 64)
 static long long warm_sum, a_sum, b_sum, bcp_sum, rounds, lanes_b, lanes_bcp, rounds_b, lanes_f, lanes_tot, sym_true;
 static long long bhist[8];
+static long long n_lit, n_match, len_sum, lhist[6], dhist[6], dfar[4];
+static int last_len;
 
 static void sim_block(int64_t p0, int64_t pend, int K, int W) {
   // true path
@@ -106,7 +108,26 @@ static void sim_block(int64_t p0, int64_t pend, int K, int W) {
     tpos[ntrue] = p;
     tst[ntrue] = (int8_t)st;
     ntrue++;
+    const int64_t q = p;
     const int k = dsym(&p, &st);
+    if (k == 0) n_lit++;
+    if (k == 1) {  // length value
+      const uint32_t b = bits_at(q);
+      const ent e = LT[b & 0x7fff];
+      const int ls = e.sym - 257;
+      last_len = LBASE[ls] + (int)((b >> e.len) & ((1u << LEXT[ls]) - 1u));
+      n_match++;
+      len_sum += last_len;
+      lhist[last_len <= 4 ? 0 : last_len <= 16 ? 1 : last_len <= 32 ? 2 : last_len <= 64 ? 3 : last_len <= 128 ? 4 : 5]++;
+    }
+    if (k == 2) {
+      const uint32_t b = bits_at(q);
+      const ent e = DT[b & 0x7fff];
+      static const uint16_t DB[30] = {1,2,3,4,5,7,9,13,17,25,33,49,65,97,129,193,257,385,513,769,1025,1537,2049,3073,4097,6145,8193,12289,16385,24577};
+      const int dv = DB[e.sym] + (int)((b >> e.len) & ((1u << DEXT[e.sym]) - 1u));
+      dhist[dv <= 4 ? 0 : dv <= 16 ? 1 : dv <= 64 ? 2 : dv <= 1024 ? 3 : dv <= 2808 ? 4 : 5]++;
+      dfar[dv <= 6904 ? 0 : dv <= 15096 ? 1 : dv <= 24000 ? 2 : 3]++;
+    }
     if (k == 3 || k == 4 || p > pend) break;
   }
   tpos[ntrue] = p;  // end (after EOB)
@@ -281,6 +302,14 @@ int main(int argc, char **argv) {
            100.0 * rounds_b / rounds);
     for (int i = 0; i < 7; i++) printf(" %lld", bhist[i]);
     printf("\n");
+    printf("tokens: lit %lld match %lld (mean len %.1f) | len <=4,<=16,<=32,<=64,<=128,>128: %lld %lld %lld %lld %lld %lld | dist <=4,<=16,<=64,<=1024,<=2808,>2808: %lld %lld %lld %lld %lld %lld\n",
+           n_lit, n_match, (double)len_sum / n_match, lhist[0], lhist[1], lhist[2], lhist[3], lhist[4], lhist[5],
+           dhist[0], dhist[1], dhist[2], dhist[3], dhist[4], dhist[5]);
+    printf("far split: <=6904 (8K ring) %lld, <=15096 (16K ring) %lld, <=24000 %lld, more %lld\n", dfar[0], dfar[1], dfar[2], dfar[3]);
+    memset(dfar, 0, sizeof dfar);
+    n_lit = n_match = len_sum = 0;
+    memset(lhist, 0, sizeof lhist);
+    memset(dhist, 0, sizeof dhist);
     fflush(stdout);
   }
   return 0;

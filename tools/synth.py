@@ -56,7 +56,8 @@ class SynthBam:
     file has no repeated tile — the large-size parity tests compare it with full oracle runs."""
 
     def __init__(self, tile_mb: float = 64.0, copies: int = 1, read_len: int = 150, seed: int = 0x5EEDBA11,
-                 level: int = 6, threads: int = 16, unplaced_mb: float | None = None, distinct: bool = False):
+                 level: int = 6, threads: int = 16, unplaced_mb: float | None = None, distinct: bool = False,
+                 cycle: int = 0):
         L = lib()
         p = ctypes.c_void_p()
         n = L.synth_header(ctypes.byref(p))
@@ -79,16 +80,20 @@ class SynthBam:
             self.tail = _take(p, n)
             self.tail_records = nrec.value
         self.distinct = distinct
+        self.cycle = cycle  # distinct: tile k is tiles[k % cycle] (0: every tile its own seed)
         self.tiles = [self.tile]
         self.tiles_records = [self.tile_records]
         self.copies = copies
         if distinct:
-            self._make_tiles(copies)
+            self._make_tiles(self._ntiles(copies))
         self._sizes()
         nr = ctypes.c_int32(0)
         lens = np.zeros(128, np.int64)
         L.synth_contigs(ctypes.byref(nr), lens.ctypes.data)
         self.contig_lengths = lens[: nr.value]
+
+    def _ntiles(self, copies: int) -> int:
+        return min(copies, self.cycle) if self.cycle > 0 else copies
 
     def _make_tiles(self, k: int):
         """Tiles 1 .. k-1 of a distinct-tile file, one generator call per worker thread (ctypes releases the GIL)."""
@@ -113,16 +118,17 @@ class SynthBam:
         s.copies = max(1, round((target_bytes - s.header.size - s.tail.size - 28) / s.tile.size))
         if distinct:
             s.distinct = True
-            s._make_tiles(s.copies)
+            s._make_tiles(s._ntiles(s.copies))
         s._sizes()
         return s
 
     def _sizes(self):
         if self.distinct:
-            sz = np.array([t.size for t in self.tiles[: self.copies]], np.int64)
+            nt = len(self.tiles)
+            sz = np.array([self.tiles[k % nt].size for k in range(self.copies)], np.int64)
             self.tile_starts = self.header.size + np.concatenate([[0], np.cumsum(sz)])
             self.body = int(self.tile_starts[-1])
-            self.n_records = int(sum(self.tiles_records[: self.copies])) + self.tail_records
+            self.n_records = int(sum(self.tiles_records[k % nt] for k in range(self.copies))) + self.tail_records
         else:
             self.body = self.header.size + self.copies * self.tile.size  # where the unplaced tail starts
             self.n_records = self.copies * self.tile_records + self.tail_records
@@ -141,7 +147,7 @@ class SynthBam:
             elif pos < self.body:
                 if self.distinct:
                     k = int(np.searchsorted(self.tile_starts, pos, side="right")) - 1
-                    tile, o = self.tiles[k], pos - int(self.tile_starts[k])
+                    tile, o = self.tiles[k % len(self.tiles)], pos - int(self.tile_starts[k])
                 else:
                     k, o = divmod(pos - H, T)
                     tile = self.tile

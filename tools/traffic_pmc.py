@@ -54,13 +54,14 @@ def main():
     ap.add_argument("--size-gb", type=float, default=10.0)
     ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EEDBA11)
     ap.add_argument("--tile-mb", type=float, default=64.0)
+    ap.add_argument("--tiles", type=int, default=16)
     a = ap.parse_args()
     fetch, nf = per_dispatch(a.fetch_dir, "FETCH_SIZE")
     write, nw = per_dispatch(a.write_dir, "WRITE_SIZE")
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "spark-bam_amd"))
     import sbam
-    out = {"workload": {"size_gb": a.size_gb, "seed": a.seed, "tile_mb": a.tile_mb},
+    out = {"workload": {"size_gb": a.size_gb, "seed": a.seed, "tile_mb": a.tile_mb, "tiles": a.tiles},
            "source_digest": sbam.source_digest(),
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes of tools/bench_kernels.py; "
                      "median dispatch; FETCH x2 (gfx950 64-B tally of 128-B requests), WRITE as reported",
