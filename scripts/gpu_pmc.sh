@@ -11,4 +11,5 @@ run f "FETCH_SIZE" || exit 2
 run w "WRITE_SIZE" || exit 3
 run sq1 "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_SMEM" || exit 4
 run sq2 "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM" || exit 5
-python3 tools/traffic_pmc.py $OUT/traffic.json $OUT/f $OUT/w --sq-dir $OUT/sq1 --sq-dir $OUT/sq2 > $OUT/summary.log 2>&1 || exit 6
+run sq3 "GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES" || exit 7
+python3 tools/traffic_pmc.py $OUT/traffic.json $OUT/f $OUT/w --sq-dir $OUT/sq1 --sq-dir $OUT/sq2 --sq-dir $OUT/sq3 > $OUT/summary.log 2>&1 || exit 6

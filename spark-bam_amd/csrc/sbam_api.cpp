@@ -69,8 +69,12 @@ struct sbam_ctx {
   bool bm_list = false;  // the bitmap came from the list-form chain pass: d_nfb[1..2] describe its links
   int32_t bm_R = -1;
   // inflate scratch: token pages of the decode → resolve path
-  uint8_t *d_pool = nullptr;  // token regions (inflate_token_bytes)
+  uint8_t *d_pool = nullptr;  // main token regions (inflate_token_bytes)
   size_t pool_cap = 0;
+  uint8_t *d_arena = nullptr;  // token arena (TokPool): blocks whose tokens outgrow their main region
+  size_t arena_cap = 0;        // bytes (the allocation has 1 KiB more: the resolver's token lookahead)
+  int64_t *d_tokbase = nullptr;
+  size_t tokbase_cap = 0;
   int32_t *d_slow = nullptr;  // blocks the wave decoder hands to the exact per-lane decoder
   size_t slow_cap = 0;
   unsigned int *d_icnt = nullptr;  // slow-path blocks, slow-path work, resolve work
@@ -291,6 +295,8 @@ void sbam_close(sbam_ctx *c) {
   dfree(c->d_lens);
   dfree(c->d_bitmap);
   dfree(c->d_pool);
+  dfree(c->d_arena);
+  dfree(c->d_tokbase);
   dfree(c->d_slow);
   dfree(c->d_icnt);
   dfree(c->d_small);
@@ -377,6 +383,11 @@ int sbam_reserve(sbam_ctx *c, int64_t comp_bytes, int64_t n_blocks, int64_t ubyt
   HIPCHK(c, ensure(&c->d_status, &c->status_cap, n_blocks));
   HIPCHK(c, ensure(&c->d_found, &c->found_cap, n_blocks));
   HIPCHK(c, ensure(&c->d_pool, &c->pool_cap, inflate_token_bytes(ubytes, n_blocks)));
+  if (inflate_arena_bytes(ubytes) > c->arena_cap) {
+    HIPCHK(c, ensure(&c->d_arena, &c->arena_cap, inflate_arena_bytes(ubytes) + 1024));
+    c->arena_cap -= 1024;
+  }
+  HIPCHK(c, ensure(&c->d_tokbase, &c->tokbase_cap, n_blocks));
   HIPCHK(c, ensure(&c->d_slow, &c->slow_cap, n_blocks));
   if (int rc = ensure_bitmap(c, 0, ubytes)) return rc;
   if (n_records > 0) {  // the chain pass's PASS0 list (about one entry per record) and loadReads' offsets
@@ -591,28 +602,57 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
   int32_t *d_status = c->d_status, *d_found = c->d_found;
   const unsigned long long none = ~0ull;
   BlockTable bt{c->d_bstart, c->d_bh, c->d_bc, c->d_bu, c->d_buoff, nb};
-  // token regions: every block's tokens at a fixed offset (at most 2 B per output byte), so no pool overflow
+  // token pool (TokPool): main regions at 1 B per output byte, the arena for blocks that need more
   HIPCHK(c, ensure(&c->d_pool, &c->pool_cap, inflate_token_bytes(L, nb)));
+  if (!c->d_arena || c->arena_cap < inflate_arena_bytes(L)) {
+    HIPCHK(c, ensure(&c->d_arena, &c->arena_cap, inflate_arena_bytes(L) + 1024));
+    c->arena_cap -= 1024;
+  }
+  HIPCHK(c, ensure(&c->d_tokbase, &c->tokbase_cap, nb));
   HIPCHK(c, ensure(&c->d_slow, &c->slow_cap, nb));
   if (!c->d_icnt) HIPCHK(c, dalloc(&c->d_icnt, 4));
-  {
-    Timer t(c, "inflate");
-    {
-      Timer t1(c, "inflate_decode");
-      HIPCHK(c, launch_inflate_decode(c->d_comp, c->D, bt, c->d_pool, d_status, d_found, c->d_slow, c->d_icnt,
-                                      c->stream));
-    }
-    Timer t2(c, "inflate_resolve");
-    HIPCHK(c, launch_inflate_resolve(bt, c->d_u, c->d_pool, d_found, c->stream));
-  }
-  HIPCHK(c, hipMemcpyAsync(c->d_small + 2, &none, 8, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, launch_first_error(d_status, nb, reinterpret_cast<unsigned long long *>(c->d_small + 2), c->stream));
+  unsigned long long *d_used = reinterpret_cast<unsigned long long *>(c->d_small + 16);
   unsigned long long ferr = 0;
-  unsigned int nslow = 0;
-  HIPCHK(c, hipMemcpyAsync(&ferr, c->d_small + 2, 8, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(&nslow, c->d_icnt, 4, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  c->inflate_slow = nslow;
+  unsigned int cnt3[3] = {0, 0, 0};  // slow-path blocks, -, blocks the resolver handed back
+  for (;;) {
+    const TokPool tp{c->d_pool, c->d_arena, (int64_t)c->arena_cap, d_used, c->d_tokbase};
+    HIPCHK(c, hipMemsetAsync(c->d_tokbase, 0xff, nb * sizeof(int64_t), c->stream));  // every block: main region
+    HIPCHK(c, hipMemsetAsync(d_used, 0, sizeof(unsigned long long), c->stream));
+    {
+      Timer t(c, "inflate");
+      {
+        Timer t1(c, "inflate_decode");
+        HIPCHK(c, launch_inflate_decode(c->d_comp, c->D, bt, tp, d_status, d_found, c->d_slow, c->d_icnt, c->stream));
+      }
+      Timer t2(c, "inflate_resolve");
+      // (the slow list is consumed by now: the resolver's redo list reuses d_slow, its count is d_icnt[2])
+      HIPCHK(c, launch_inflate_resolve(bt, c->d_u, tp, d_found, nullptr, 0, c->d_slow, c->d_icnt + 2, c->stream));
+    }
+    HIPCHK(c, hipMemcpyAsync(c->d_small + 2, &none, 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, launch_first_error(d_status, nb, reinterpret_cast<unsigned long long *>(c->d_small + 2), c->stream));
+    HIPCHK(c, hipMemcpyAsync(&ferr, c->d_small + 2, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(cnt3, c->d_icnt, 12, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (cnt3[2] > 0) {  // a distance past its block's start ("invalid distance too far back"): the exact decoder
+      HIPCHK(c, launch_inflate_redo(c->d_comp, c->D, bt, tp, c->d_slow, c->d_icnt, d_status, d_found, c->stream));
+      HIPCHK(c, launch_inflate_resolve(bt, c->d_u, tp, d_found, c->d_slow, cnt3[2], nullptr, nullptr, c->stream));
+      HIPCHK(c, hipMemcpyAsync(c->d_small + 2, &none, 8, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, launch_first_error(d_status, nb, reinterpret_cast<unsigned long long *>(c->d_small + 2), c->stream));
+      HIPCHK(c, hipMemcpyAsync(&ferr, c->d_small + 2, 8, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    if (ferr == ~0ull) break;
+    int32_t st = 0;
+    unsigned long long used = 0;
+    HIPCHK(c, hipMemcpy(&st, d_status + ferr, 4, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(&used, d_used, 8, hipMemcpyDeviceToHost));
+    if (st != 3 /* INF_OVERFLOW */ || used <= c->arena_cap) break;
+    // the arena was too small for the blocks that needed it (used counts every request): grow it, inflate again
+    if (log_grow()) std::fprintf(stderr, "[sbam] token arena %zu -> %llu bytes\n", c->arena_cap, used);
+    HIPCHK(c, ensure(&c->d_arena, &c->arena_cap, (size_t)used + (used >> 3) + 1024));
+    c->arena_cap -= 1024;
+  }
+  c->inflate_slow = cnt3[0] + cnt3[2];
   if (ferr != ~0ull) {
     int32_t found = 0;
     HIPCHK(c, hipMemcpy(&found, d_found + ferr, 4, hipMemcpyDeviceToHost));

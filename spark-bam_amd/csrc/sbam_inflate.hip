@@ -30,11 +30,15 @@ enum : int32_t { INF_OK = 0, INF_SHORT = 1, INF_DATA = 2, INF_OVERFLOW = 3 };
 constexpr uint32_t kTokPad = 0x7fffu;
 constexpr uint32_t kTokDist = 0x8000u;
 
-// Block b's tokens are u16s in the 16-B aligned region tok_region(uoff[b], b) of the token buffer.  A block yields
-// at most ISIZE tokens plus 7 of padding (slow decoder), and regions 2 uoff + 32 b apart never overlap.
+// Block b's main token region: the 16-B aligned region tok_region(uoff[b], b) of TokPool::main, 1 B per uncompressed
+// byte (+ 32 B per block): room for (usize + 16) / 2 tokens (a token stands for >= 1 output byte, and the synthetic
+// BAM needs 0.74 B per byte).  A block that needs more (up to ISIZE tokens plus 7 of padding) takes 2 ISIZE + 32 B
+// of the arena (TokPool).
 SB_DEV uint64_t tok_region(int64_t uoff, int64_t b) {
-  return (((uint64_t)uoff * 2 + 15) & ~15ull) + 32ull * (uint64_t)b;
+  return (((uint64_t)uoff + 15) & ~15ull) + 32ull * (uint64_t)b;
 }
+SB_DEV int32_t tok_region_cap(int32_t us) { return (us + 16) / 2; }  // tokens
+SB_DEV uint64_t tok_arena_need(int32_t us) { return ((uint64_t)(2 * us + 32) + 15) & ~15ull; }
 
 // ---- decode kernel --------------------------------------------------------------------------------------------
 // Per-lane tables live in LDS, interleaved across the workgroup's lanes at dword granularity (byte b of lane L at
@@ -272,7 +276,7 @@ struct Bits {
 };
 
 __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *__restrict__ d, int64_t D,
-                                                                 BlockTable bt, uint8_t *__restrict__ pool,
+                                                                 BlockTable bt, TokPool tp,
                                                                  const int32_t *__restrict__ slow,
                                                                  const unsigned int *nslow,
                                                                  int32_t *__restrict__ status,
@@ -281,6 +285,7 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
   __shared__ __attribute__((aligned(16))) uint8_t s_dec[kRows * kDecThreads * 4];
   const Slice sl{s_dec + 4 * threadIdx.x};
   const uint32_t *d32 = reinterpret_cast<const uint32_t *>(d);
+  uint8_t *pool = tp.arena;  // every block of this decoder writes into an arena region of its own
 
   int state = S_NEXT;
   int64_t blk = -1;
@@ -327,8 +332,14 @@ __global__ __launch_bounds__(kDecThreads, 2) void k_inflate_slow(const uint8_t *
           err = INF_DATA;
           state = S_DONE;
         } else {
-          {
-            to.cur = tok_region(bt.uoff[blk], blk);
+          const uint64_t need = tok_arena_need(us);
+          const uint64_t at = atomicAdd(tp.arena_used, (unsigned long long)need);
+          if ((int64_t)(at + need) > tp.arena_cap) {
+            err = INF_OVERFLOW;  // the host grows the arena and inflates again
+            state = S_DONE;
+          } else {
+            tp.base[blk] = (int64_t)at;
+            to.cur = at;
             to.n = 0;
             to.pend = false;
             // word pointer derived from d by arithmetic only (an integer round trip would make it a flat
@@ -761,8 +772,8 @@ constexpr int kWarm = SBAM_WARM;
 // common case after the warm-up) then only stores them in phase C; it decodes again only past step kTR.  With the
 // round-3 v2 step (38 VALU instead of 58) the register budget is what limits kTR: 96 tokens spilled 48 VGPRs to
 // scratch, 80 spill 11 (decode at 10 GB: 96 → 47.7 ms, 80 → 45.9; 72: 47.5, its phase C re-decodes more tails).
-#ifndef SBAM_CHK_SLACK  // (0 reproduces the round-3 gate: tests/test_inflate_streams.py::test_inflate_round_boundary_distance)
-#define SBAM_CHK_SLACK 258
+#ifndef SBAM_WPRE  // next-window prefetch into registers (WinPre): 1 during phase C, 2 during the table build
+#define SBAM_WPRE 0
 #endif
 #ifndef SBAM_TR
 #define SBAM_TR 80
@@ -1010,6 +1021,41 @@ SB_DEV void wave_stage(uint32_t *win, const uint32_t *base, int64_t base_dw, int
   }
   __syncthreads();
 }
+// The same window loaded into registers ahead of time (WinPre::fetch as soon as the next window's start is known:
+// after phase B for the next round or block header, after the header for the first round), stored into LDS when
+// the window is free (WinPre::stage): the loads' latency hides behind phase C or the table build.
+struct WinPre {
+  static constexpr int kN = (wd::kWinDw + 255) / 256;
+  uint4 v[kN];
+  int wq = -1;  // window start (dwords) of v, or -1
+  SB_DEV void fetch(const uint32_t *base, int64_t base_dw, int wq_dw, int64_t lim_dw) {
+    const int lane = (int)threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < kN; k++) {
+      const int i = lane * 4 + 256 * k;
+      const int64_t g = base_dw + wq_dw + i;
+      v[k] = (i < wd::kWinDw && g + 4 <= lim_dw) ? *reinterpret_cast<const uint4 *>(base + wq_dw + i)
+                                                   : make_uint4(0, 0, 0, 0);
+    }
+    wq = wq_dw;
+  }
+  // stage window wq_dw: from the registers when they hold it, else loaded now
+  SB_DEV void stage(uint32_t *win, const uint32_t *base, int64_t base_dw, int wq_dw, int64_t lim_dw) {
+    if (SBAM_WPRE && wq == wq_dw) {
+      const int lane = (int)threadIdx.x;
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < kN; k++) {
+        const int i = lane * 4 + 256 * k;
+        if (i < wd::kWinDw) *reinterpret_cast<uint4 *>(win + i) = v[k];
+      }
+      __syncthreads();
+    } else {
+      wave_stage(win, base, base_dw, wq_dw, lim_dw);
+    }
+    wq = -1;
+  }
+};
 
 // Result of one lane's decode of its segment from a given start: counts, exit key (pos << 10 | state << 9 |
 // pending length) and stop.
@@ -1038,7 +1084,7 @@ extern "C" int sbam_debug_wave_stats(unsigned long long *out, int reset) {
 #endif
 
 __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restrict__ d, int64_t D, BlockTable bt,
-                                                     uint8_t *__restrict__ pool, int32_t *__restrict__ status,
+                                                     TokPool tp, int32_t *__restrict__ status,
                                                      int32_t *__restrict__ found, int32_t *__restrict__ slow,
                                                      unsigned int *nslow) {
   using namespace wd;
@@ -1061,7 +1107,8 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
   const int64_t lim_dw = (D + kCompPad) >> 2;
   const int skip = (int)(a - base_dw * 4) * 8;
   const int pend = skip + 8 * dlen;  // payload end (bits)
-  uint8_t *reg = pool + tok_region(bt.uoff[b], b);
+  uint8_t *reg = tp.main + tok_region(bt.uoff[b], b);
+  int32_t tcap = tok_region_cap(us);  // tokens the region holds (the arena region: all a block can produce)
   uint8_t *lens = L.lens();
   int pos = skip;
   int out = 0, ntok = 0;
@@ -1072,10 +1119,11 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
   const uint64_t wt0_ = wt_;
 #endif
 
+  WinPre pre;
   for (bool fin = false; ok && !fin;) {
     // ---- block header
     int wq = (pos >> 7) << 7;
-    wave_stage(L.win, base, base_dw, wq >> 5, lim_dw);
+    pre.stage(L.win, base, base_dw, wq >> 5, lim_dw);
     WMARK(12);
     if (pos + 3 > pend) { ok = false; break; }
     HBits h;
@@ -1225,6 +1273,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
     if (h.pos > pend) { ok = false; break; }
     WMARK(0);
     WADD(9, 1);
+    if (SBAM_WPRE & 2) pre.fetch(base, base_dw, (h.pos >> 7) << 2, lim_dw);  // the first round's window, during the build
     if (!wave_build<true>(L, 288, hdist, kDistSubOff, kDistSub)) { ok = false; break; }
     if (!wave_build<false>(L, 0, hlit, kLitSubOff, kLitSub)) { ok = false; break; }
     WMARK(1);
@@ -1234,7 +1283,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
     for (;;) {
       const int Sp = (int)(S >> 10);
       wq = (Sp >> 7) << 7;
-      wave_stage(L.win, base, base_dw, wq >> 5, lim_dw);
+      pre.stage(L.win, base, base_dw, wq >> 5, lim_dw);
       const uint32_t *wp = L.win - (wq >> 5);  // wp[pos >> 5]: the staged dword holding bit pos
       WMARK(2);
       WADD(6, 1);
@@ -1251,7 +1300,6 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       uint32_t tokA = 0, bytA = 0, exitEnd, entry;
       uint32_t tr[kTR / 2];  // phase-A tokens of steps [0, kTR)
       uint32_t stR = 0, bytR = 0;  // state (exit key) and bytes after step kTR
-      int slack = 1 << 30;  // min over the phase-A path's distances of (local bytes before the match - distance)
       {
         uint32_t st4 = lane == 0 ? (S >> 7) & 4u : 0u;  // state << 2 (the table's byte offset for the state)
         uint32_t pl = lane == 0 ? (S & 511u) : 0u;
@@ -1291,13 +1339,6 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
           wC = q[2];
         }
 #endif
-        // 0x7fff + local bytes before the pending match (a distance d = token - 0x7fff is too far back for the path
-        // when this minus the token is below -o0)
-        uint32_t bq = 0x7fffu - pl;
-        bool first = nst == 0;  // no stop yet
-        // o0 >= out and a distance is at most 32768, but a lane (or round) that starts in the distance state has
-        // its match begin pl <= 258 bytes before o0: from out >= 32768 + 258 on no distance reaches past the start
-        const bool chk = out < 32768 + SBAM_CHK_SLACK;
         // one symbol, predicated: a lane that is done (stopped out of the data, or past its segment) decodes the
         // same symbol again and commits nothing, so the steps need no exec-mask branches
         // ST: the step's index when it is below kTR (its token goes to tr), else -1
@@ -1325,7 +1366,6 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
             s2e = w2 ? ek : s2e;
             s2c = w2 ? cn : s2c;
             nst += stp ? 1 : 0;
-            first = first && !stp;
             go = (stp && outp) ? false : go;
           }
           rp = live ? rq : rp;
@@ -1345,15 +1385,10 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
               tr[sj / 2] = __builtin_amdgcn_perm(v, tr[sj / 2], 0x05040100u);  // low half kept, v above
             }
           }
-          // selects and carry-in adds only (no exec-mask branches): counts, pending length, and the path's distance
-          // check (zlib "invalid distance too far back") up to its first stop
+          // selects and carry-in adds only (no exec-mask branches): counts and the pending length.  (zlib's
+          // "invalid distance too far back" is the resolver's test: k_inflate_resolve hands such a block back.)
           const bool cl = cnt && kind == K_LEN;
           const uint32_t lenv = v - 253u;
-          if (chk) {  // (wave-uniform: from 32 KiB of block output on, no distance reaches back past its start)
-            const int sx = min(slack, (int)(bq - v));
-            slack = (cnt && first && kind == K_DIST) ? sx : slack;
-            bq = cl ? bytA + 0x7fffu : bq;
-          }
           tokA += cnt ? 1u : 0u;                                        // (v_addc with the lane mask as carry-in)
           bytA += (cl ? lenv : 0u) + ((cnt && kind == K_LIT) ? 1u : 0u);  // + length, or + 1 for a literal
           pl = cl ? lenv : pl;
@@ -1395,11 +1430,11 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       uint32_t bst = lane == 0 ? S : entry;
       bool ver = lane == 0;
       // where phase C finds the lane's tokens: kModeA — res is phase A's own result (tokens in tr from step 0);
-      // kModeR — re-decoded from the true start up to phase A's checkpoint rjP (rjtk tokens, rjby bytes), then
-      // phase A's path from step rjs (rjcb: phase A's bytes at the checkpoint); kModeF — re-decoded to the end
+      // kModeR — re-decoded from the true start up to phase A's checkpoint rjP (rjtk tokens), then phase A's path
+      // from step rjs; kModeF — re-decoded to the end
       enum : int { kModeA = 0, kModeR = 1, kModeF = 2 };
       int mode = kModeA;
-      uint32_t rjP = 0, rjs = 0, rjtk = 0, rjby = 0, rjcb = 0;
+      uint32_t rjP = 0, rjs = 0, rjtk = 0;
       int f = 64;
       for (;;) {
         uint32_t pex = __shfl_up(nxt, 1);
@@ -1445,8 +1480,6 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
               rjP = P;
               rjs = sj;
               rjtk = tk;
-              rjby = by;
-              rjcb = cj >> 12;
               // the first recorded stop at or after the checkpoint ends the path
               const bool h1 = nst >= 1 && s1p >= P, h2 = !h1 && nst >= 2 && s2p >= P;
               if (h1 || h2) {
@@ -1485,6 +1518,9 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         }
       }
       WMARK(4);
+      // the next window's start (the next round's, or the next block header's) is known now
+      const int next_wq = (f < 64 ? (int)(uni((uint32_t)__shfl(res.exit, f)) >> 10)
+                                  : (int)(uni((uint32_t)__shfl(nxt, 63)) >> 10)) >> 7 << 2;
       // lanes 0..f carry the true path (f: the lane whose segment ends the deflate block, or 64)
       const bool act = lane <= f;
 #ifdef SBAM_WAVE_STATS
@@ -1510,28 +1546,43 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         ok = false;
         break;
       }
+      if (ntok + (int)tot_tok > tcap) {  // (rare) the block outgrows its main region: move its tokens to the arena
+        const uint64_t need = tok_arena_need(us);
+        uint64_t at = 0;
+        if (lane == 0) at = atomicAdd(tp.arena_used, (unsigned long long)need);
+        at = ((uint64_t)uni((uint32_t)__shfl((int)(at >> 32), 0)) << 32) | uni((uint32_t)__shfl((int)(uint32_t)at, 0));
+        if ((int64_t)(at + need) > tp.arena_cap) {  // the exact decoder reports the overflow; the host grows the arena
+          ok = false;
+          break;
+        }
+        uint8_t *nreg = tp.arena + at;
+        __threadfence();  // the earlier rounds' token stores are visible to the copy's loads
+        const int nb = 2 * ntok, nb16 = nb & ~15;
+        for (int i = 16 * lane; i < nb16; i += 1024)
+          *reinterpret_cast<uint4 *>(nreg + i) = *reinterpret_cast<const uint4 *>(reg + i);
+        if (lane < (nb - nb16) / 2)
+          reinterpret_cast<uint16_t *>(nreg + nb16)[lane] = reinterpret_cast<const uint16_t *>(reg + nb16)[lane];
+        if (lane == 0) tp.base[b] = (int64_t)at;
+        reg = nreg;
+        tcap = 1 << 30;
+      }
       // ---- phase C: write the true segments' tokens at their offsets.  A lane re-decodes only what phase A's
       // registers do not hold: mode F its whole segment, mode R the stretch up to its rejoin checkpoint; then the
       // register tokens; then whatever lies past step kTR.
-      bool derr = false;
+      bool tail = false;
+      uint32_t tail_ti = 0;
       if (act) {
         uint32_t start = __shfl_up(nxt, 1);
         if (lane == 0) start = S;
-        const int o0 = out + (int)(ibyt - my_byt);
-        int o = o0;
         uint32_t ti = (uint32_t)ntok + (itok - my_tok);
         // decode from key st until the reader reaches endp (or the end-of-block symbol of lane f), writing tokens
         auto run = [&](uint32_t st, int endp) {
           uint32_t st4 = (st >> 7) & 4u;
-          uint32_t pl = st & 511u;
           int rp = (int)(st >> 10);
           while (rp < endp) {
             uint32_t v;
             const uint32_t kind = wsym(wp, L, rp, st4, v);
             if (kind == K_SPEC) break;
-            if (kind == K_DIST) derr |= (int)(v - 0x7fffu) > o - (int)pl;  // v: the token
-            o += kind == K_LIT ? 1 : kind == K_LEN ? (int)v - 253 : 0;
-            pl = kind == K_LEN ? v - 253u : pl;
             st4 = kind == K_LEN ? 4u : 0u;
             *reinterpret_cast<uint16_t *>(reg + 2 * ti) = (uint16_t)v;
             ti++;
@@ -1540,20 +1591,19 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         WMARK(24);
         run(start, mode == kModeF ? seg_end : mode == kModeR ? (int)rjP : 0);
         WMARK(25);
-        // register tokens [lo, hi) of phase A's path
+        // register tokens [lo, hi) of phase A's path (mode A: from step 0; mode R: from its rejoin checkpoint's
+        // step), token k at index tb + k
         const uint32_t lo = mode == kModeR ? rjs : 0u;
         const uint32_t n = mode == kModeA ? res.tok : mode == kModeR ? res.tok - rjtk : 0u;
-        const uint32_t hi = min(lo + n, (uint32_t)kTR);
-        uint16_t *dst = reinterpret_cast<uint16_t *>(reg) + ti - lo;
-        derr |= mode == kModeA && o0 + slack < 0;  // the path's distances, checked as phase A went
+        const uint32_t hi = mode == kModeF ? 0u : min(lo + n, (uint32_t)kTR);
+        const uint32_t tb = ti - lo;
         {
-          // mode A: register tokens [0, hi) at token index ti, as 16-B stores (4-B aligned: a 2-B head when ti is
-          // odd), then 4-B and a last 2-B store — a lane's run is contiguous, so 8 tokens per store instruction
-          // instead of one (every store instruction writes 64 lanes' separate lines)
-          const uint32_t na = mode == kModeA ? hi : 0u;
-          const uint32_t par = ti & 1u;
-          uint8_t *pa = reg + 2 * (uint64_t)ti;
-          if (par && na) *reinterpret_cast<uint16_t *>(pa) = (uint16_t)tr[0];
+          // 16-B stores (4-B aligned: a 2-B head when tb is odd), dwords and 2-B halves where the run starts or ends
+          // inside a chunk — a lane's run is contiguous, so 8 tokens per store instruction instead of one (every
+          // store instruction writes 64 lanes' separate lines)
+          const uint32_t par = tb & 1u;
+          uint8_t *pa = reg + 2 * ((int64_t)ti - (int64_t)lo);  // (tb may lie before the region: only k >= lo is stored)
+          if (par && lo == 0 && hi > 0) *reinterpret_cast<uint16_t *>(pa) = (uint16_t)tr[0];
           u32x4a *pv = reinterpret_cast<u32x4a *>(pa + 2 * par);
           uint32_t *pw = reinterpret_cast<uint32_t *>(pa + 2 * par);
           // dword q: tokens par + 2q, par + 2q + 1
@@ -1566,43 +1616,44 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
             constexpr int c = decltype(C)::value;
             const uint32_t a0 = dw(std::integral_constant<int, 4 * c>{}), a1 = dw(std::integral_constant<int, 4 * c + 1>{});
             const uint32_t a2 = dw(std::integral_constant<int, 4 * c + 2>{}), a3 = dw(std::integral_constant<int, 4 * c + 3>{});
-            if (par + 8 * c + 8 <= na) {
+            const uint32_t t0 = par + 8 * c;  // the chunk's first token
+            if (t0 >= lo && t0 + 8 <= hi) {
               pv[c] = u32x4a{a0, a1, a2, a3};
-            } else if (par + 8 * c < na) {  // the run ends in this chunk: dwords, then a last single token
+            } else if (t0 + 8 > lo && t0 < hi) {  // the run starts or ends in this chunk
               const uint32_t a[4] = {a0, a1, a2, a3};
 #pragma unroll
               for (int k = 0; k < 4; k++) {
-                if (par + 8 * c + 2 * k + 2 <= na) pw[4 * c + k] = a[k];
-                else if (par + 8 * c + 2 * k + 1 == na) *reinterpret_cast<uint16_t *>(pw + 4 * c + k) = (uint16_t)a[k];
+                const uint32_t u0 = t0 + 2 * k;
+                const bool in0 = u0 >= lo && u0 < hi, in1 = u0 + 1 >= lo && u0 + 1 < hi;
+                uint16_t *ph = reinterpret_cast<uint16_t *>(pw + 4 * c + k);
+                if (in0 && in1) pw[4 * c + k] = a[k];
+                else if (in0) ph[0] = (uint16_t)a[k];
+                else if (in1) ph[1] = (uint16_t)(a[k] >> 16);
               }
             }
           });
         }
         WMARK(26);
-        if (__ballot(mode == kModeR) != 0) {  // mode R's path starts mid-way through phase A's: check its distances
-          int od = o;
-          uint32_t pd = 0;
-          const bool chk = mode == kModeR;
-          sfor<0, kTR>([&](auto K) {
-            constexpr int k = decltype(K)::value;
-            if ((uint32_t)k >= lo && (uint32_t)k < hi) {
-              const uint32_t t = (tr[k / 2] >> (16 * (k & 1))) & 0xffffu;
-              dst[k] = (uint16_t)t;
-              derr |= chk && t > 0x7fffu && (int)(t - 0x7fffu) > od - (int)pd;
-              od += t < 256u ? 1 : t < 512u ? (int)t - 253 : 0;
-              pd = (t >> 8) == 1u ? t - 253u : pd;
-            }
-          });
-        }
         WMARK(27);
-        if (mode != kModeF && lo + n > (uint32_t)kTR) {  // the path goes on past step kTR (no stop before it)
-          ti = ti - lo + kTR;
-          o = o0 + (int)(mode == kModeA ? bytR : rjby + bytR - rjcb);
-          run(stR, seg_end);
+        tail = mode != kModeF && lo + n > (uint32_t)kTR;  // the path goes on past step kTR (no stop before it)
+        ti = tb + kTR;
+        tail_ti = ti;
+      }
+      // the register tokens are stored: their VGPRs take the next window's loads, which the tail decode hides
+      if (SBAM_WPRE & 1) pre.fetch(base, base_dw, next_wq, lim_dw);
+      if (tail) {
+        uint32_t st4 = (stR >> 7) & 4u, ti = tail_ti;
+        int rp = (int)(stR >> 10);
+        while (rp < seg_end) {
+          uint32_t v;
+          const uint32_t kind = wsym(wp, L, rp, st4, v);
+          if (kind == K_SPEC) break;
+          st4 = kind == K_LEN ? 4u : 0u;
+          *reinterpret_cast<uint16_t *>(reg + 2 * ti) = (uint16_t)v;
+          ti++;
         }
       }
       WMARK(28);
-      if (__ballot(derr) != 0) { ok = false; break; }
       out += (int)tot_byt;
       ntok += (int)tot_tok;
       if (f < 64) {  // end of block: the next header follows lane f's end-of-block symbol
@@ -1645,11 +1696,11 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
 // A block's LZ77 window never leaves the chip except for the far copies; HBM sees the words once and the output
 // once.  (Round 2; the round-1 design ran one lane per block with the window in HBM and was bound by the memory
 // side: 16.5x the output bytes per launch.)
-#ifndef SBAM_RESOLVE4
-#define SBAM_RESOLVE4 0
-#endif
-#ifndef SBAM_FAR_DEFER  // far copies wait until the first pending match is far (their loads overlap the near rounds)
-#define SBAM_FAR_DEFER 1
+// SBAM_FAR_DEFER=1: far copies wait until the first pending match is far, so their loads overlap the near rounds.
+// Round 4 A/B at 10 GB: 41.2 ms with, 38.7 ms without (the deferred far copies added rounds).  (Also tried in round
+// 4: four tokens per lane per step, to halve the per-step overhead: 46.2 ms deferred / 42.1 not — slower.)
+#ifndef SBAM_FAR_DEFER
+#define SBAM_FAR_DEFER 0
 #endif
 namespace rs {
 constexpr int kSpan = 1024;   // a chunk's words start within kSpan bytes of its base
@@ -1696,10 +1747,15 @@ SB_DEV void ring_or5(uint32_t *ring, uint32_t q, uint32_t w0, uint32_t w1, uint3
   }
 }
 
+// zlib's "invalid distance too far back" (a match reaching before the block's first output byte) is detected here,
+// where every match's output position is known: the decoder's speculative phases never test it.  Such a block is
+// listed in redo[] (nothing is read before its output) and the host hands it to k_inflate_slow, which reports the
+// error with zlib's count, then resolves it again (list: the blocks of that second pass).
 template <int RB>
-__global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *__restrict__ out,
-                                                        const uint8_t *__restrict__ pool,
-                                                        const int32_t *__restrict__ found) {
+__global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *__restrict__ out, TokPool pool,
+                                                        const int32_t *__restrict__ found,
+                                                        const int32_t *__restrict__ list, int32_t *__restrict__ redo,
+                                                        unsigned int *__restrict__ nredo) {
   using G = RingGeom<RB>;
   __shared__ __attribute__((aligned(16))) uint32_t ring[G::kDw + G::kMirror];
   __shared__ __attribute__((aligned(16))) uint32_t s_keep[17 * 4];  // s_keep[4n..4n+3]: mask of the low n bytes
@@ -1709,18 +1765,21 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
     const int n = i >> 2, k = i & 3, nb = n - 4 * k;  // bytes of dword k kept
     s_keep[i] = nb >= 4 ? ~0u : nb <= 0 ? 0u : (1u << (8 * nb)) - 1u;
   }
-  const int64_t b = blockIdx.x;
+  const int64_t b = list ? list[blockIdx.x] : blockIdx.x;
   const int ae = found[b];  // output bytes of the block
   if (ae <= 0) return;
   const int64_t U0 = bt.uoff[b];
   uint8_t *ob = out + U0;
   const uint32_t Gr = (uint32_t)U0 & G::kMask;  // ring byte of position 0
-  const uint16_t *tk = reinterpret_cast<const uint16_t *>(pool + tok_region(U0, b));
+  const int64_t tbase = pool.base[b];
+  const uint16_t *tk =
+      reinterpret_cast<const uint16_t *>(tbase >= 0 ? pool.arena + tbase : pool.main + tok_region(U0, b));
   const int F0 = (int)((16 - (U0 & 15)) & 15);  // first position on a 16-B boundary
   int F = F0;                                     // flushed up to here (from F0)
   bool head = F0 == 0;                            // positions [0, F0) stored
   int Z = -(int)(Gr & 3u);                        // ring zeroed for positions [.., Z); Gr + Z is dword aligned
   int B = 0, tp = 0;                              // chunk base position, its first token
+  bool toofar = false;                            // a distance past the block's first byte (zlib: data error)
   // lane i holds tokens tp + 2i and tp + 2i + 1, and sees tp + 2i + 2 (the distance of a length in its second)
   uint32_t ta = tk[2 * lane], tb = tk[2 * lane + 1], tn = tk[2 * lane + 2];
   while (B < ae) {
@@ -1770,7 +1829,10 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
     }
     // ---- 3b. matches, in rounds
     const int mO = O + (bLen ? nl : 0);
-    const int Le = (take && Lm > 0) ? min(Lm, ae - mO) : 0;
+    int Le = (take && Lm > 0) ? min(Lm, ae - mO) : 0;
+    const bool tf = Le > 0 && d > mO;  // invalid distance too far back: no copy, the block goes to the exact decoder
+    toofar |= tf;
+    Le = tf ? 0 : Le;
     const bool mt = Le > 0;
     const bool far = d > G::kNear;
     const int srcEnd = mO - d + min(Le, d);
@@ -1860,217 +1922,7 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
       *reinterpret_cast<uint4 *>(ob + p) = *reinterpret_cast<const uint4 *>(ring8 + ((Gr + (uint32_t)p) & G::kMask));
     if (Ft + lane < ae) ob[Ft + lane] = ring8[(Gr + (uint32_t)(Ft + lane)) & G::kMask];
   }
-}
-
-// ---- resolve, four tokens per lane (round 4) -------------------------------------------------------------------
-// The same ring, masks and dependency rounds as k_inflate_resolve, but a step takes 256 tokens (four per lane): the
-// step's fixed work — prefix sum, ring zeroing, round heads, token loads, flush checks — is paid once per ≈ 690 output
-// bytes instead of ≈ 345 (token statistics of the synthetic BAM: 61 % literals, matches of 7.7 bytes on average, 44 %
-// of distances past the ring's near window).  A lane yields up to four literals and up to two matches (slot A: its
-// first length token, slot B: its second; a length in its last token takes the next lane's first token as its
-// distance).  A round's order is (lane, slot): the first pending match is always ready, and a match is ready when its
-// source ends at or before that match's output, or when the nearest pending match before it (slot A of the same lane
-// for slot B, else the last pending slot of the nearest lane below) ends at or before its source starts.
-namespace rs4 {
-struct Match {
-  int mO, d, Le, srcEnd;
-  bool far;
-};
-}  // namespace rs4
-
-template <int RB>
-__global__ __launch_bounds__(64) void k_inflate_resolve4(BlockTable bt, uint8_t *__restrict__ out,
-                                                         const uint8_t *__restrict__ pool,
-                                                         const int32_t *__restrict__ found) {
-  using G = RingGeom<RB>;
-  __shared__ __attribute__((aligned(16))) uint32_t ring[G::kDw + G::kMirror];
-  __shared__ __attribute__((aligned(16))) uint32_t s_keep[17 * 4];  // s_keep[4n..4n+3]: mask of the low n bytes
-  uint8_t *ring8 = reinterpret_cast<uint8_t *>(ring);
-  const int lane = (int)threadIdx.x;
-  for (int i = lane; i < 17 * 4; i += 64) {
-    const int n = i >> 2, k = i & 3, nb = n - 4 * k;  // bytes of dword k kept
-    s_keep[i] = nb >= 4 ? ~0u : nb <= 0 ? 0u : (1u << (8 * nb)) - 1u;
-  }
-  const int64_t b = blockIdx.x;
-  const int ae = found[b];  // output bytes of the block
-  if (ae <= 0) return;
-  const int64_t U0 = bt.uoff[b];
-  uint8_t *ob = out + U0;
-  const uint32_t Gr = (uint32_t)U0 & G::kMask;  // ring byte of position 0
-  const uint16_t *tk = reinterpret_cast<const uint16_t *>(pool + tok_region(U0, b));
-  const int F0 = (int)((16 - (U0 & 15)) & 15);  // first position on a 16-B boundary
-  int F = F0;                                     // flushed up to here (from F0)
-  bool head = F0 == 0;                            // positions [0, F0) stored
-  int Z = -(int)(Gr & 3u);                        // ring zeroed for positions [.., Z); Gr + Z is dword aligned
-  int B = 0, tp = 0;                              // step base position, its first token
-  const uint64_t below = (1ull << lane) - 1ull;
-  // lane i holds tokens tp + 4i .. tp + 4i + 3 and sees tp + 4i + 4 (the distance of a length in its last token)
-  uint32_t t0 = tk[4 * lane], t1 = tk[4 * lane + 1], t2 = tk[4 * lane + 2], t3 = tk[4 * lane + 3],
-           tn = tk[4 * lane + 4];
-  while (B < ae) {
-    // ---- 1. positions
-    const bool l0 = t0 < 256u, l1 = t1 < 256u, l2 = t2 < 256u, l3 = t3 < 256u;
-    const bool L0 = (t0 >> 8) == 1u, L1 = (t1 >> 8) == 1u, L2 = (t2 >> 8) == 1u, L3 = (t3 >> 8) == 1u;
-    const int w0 = l0 ? 1 : L0 ? (int)t0 - 253 : 0, w1 = l1 ? 1 : L1 ? (int)t1 - 253 : 0;
-    const int w2 = l2 ? 1 : L2 ? (int)t2 - 253 : 0, w3 = l3 ? 1 : L3 ? (int)t3 - 253 : 0;
-    const int c1 = w0, c2 = c1 + w1, c3 = c2 + w2, Ln = c3 + w3;
-    const int incl = (int)wave_incl_scan((uint32_t)Ln);
-    const int ex = incl - Ln;
-    const int O = B + ex;
-    const bool take = ex < rs::kSpan && O < ae;
-    const uint64_t tmask = __ballot(take);
-    const int nt = __popcll(tmask);  // a prefix of the lanes (lane 0 always)
-    const int E = min(B + __builtin_amdgcn_readlane(incl, nt - 1), ae);
-    if (E <= B) break;  // (no output left in the tokens: never for a decoded stream)
-    // the next step starts after the last taken lane's tokens (and the distance its last token may own)
-    const int tp2 = uni(tp + 4 * nt + (int)((__ballot(L3) >> (nt - 1)) & 1ull));
-    // ---- 2. zero the ring dwords of [Z, E)
-    {
-      const uint32_t z0 = (Gr + (uint32_t)Z) >> 2, z1 = (Gr + (uint32_t)E + 3u) >> 2;
-#pragma unroll 1
-      for (uint32_t k0 = z0; k0 < z1; k0 += 64u) {  // (usually one to three rounds)
-        const uint32_t k = k0 + (uint32_t)lane, i = k & G::kDwMask;
-        if (k < z1) {
-          ring[i] = 0u;
-          if (i < G::kMirror) ring[G::kDw + i] = 0u;
-        }
-      }
-      Z = (int)(z1 * 4u - Gr);
-    }
-    // ---- 3a. literals (byte stores: lanes writing neighbouring bytes of one dword never race)
-    if (take) {
-      auto lit = [&](bool isl, uint32_t t, int c) {
-        if (isl && O + c < ae) {
-          const uint32_t x = (Gr + (uint32_t)(O + c)) & G::kMask;
-          ring8[x] = (uint8_t)t;
-          if (x < 4u * G::kMirror) ring8[G::kRing + x] = (uint8_t)t;
-        }
-      };
-      lit(l0, t0, 0);
-      lit(l1, t1, c1);
-      lit(l2, t2, c2);
-      lit(l3, t3, c3);
-    }
-    // ---- 3b. matches: slot A (first length token of the lane), slot B (second)
-    const uint32_t tdA = L0 ? t1 : L1 ? t2 : L2 ? t3 : tn;
-    const int cA = L0 ? 0 : L1 ? c1 : L2 ? c2 : c3;
-    const int lenA = L0 ? w0 : L1 ? w1 : L2 ? w2 : L3 ? w3 : 0;
-    const bool hasB = (L0 && (L2 || L3)) || (L1 && L3);
-    const uint32_t tdB = (L0 && L2) ? t3 : tn;
-    const int cB = (L0 && L2) ? c2 : c3;
-    const int lenB = hasB ? ((L0 && L2) ? w2 : w3) : 0;
-    rs4::Match mA, mB;
-    mA.mO = O + cA;
-    mA.d = (int)(tdA & 0x7fffu) + 1;
-    mA.Le = (take && lenA > 0) ? min(lenA, ae - mA.mO) : 0;
-    mA.far = mA.d > G::kNear;
-    mA.srcEnd = mA.mO - mA.d + min(mA.Le, mA.d);
-    mB.mO = O + cB;
-    mB.d = (int)(tdB & 0x7fffu) + 1;
-    mB.Le = (take && lenB > 0) ? min(lenB, ae - mB.mO) : 0;
-    mB.far = mB.d > G::kNear;
-    mB.srcEnd = mB.mO - mB.d + min(mB.Le, mB.d);
-    const bool mtA = mA.Le > 0, mtB = mB.Le > 0;
-    // far sources (already in HBM, final) are loaded now, their first 16 B; their copies wait until a near copy
-    // needs them (the first pending match is far), so the loads overlap the near rounds
-    u32x4 pfA = {0u, 0u, 0u, 0u}, pfB = {0u, 0u, 0u, 0u};
-    if (mtA && mA.far) pfA = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(ob + mA.mO - mA.d));
-    if (mtB && mB.far) pfB = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(ob + mB.mO - mB.d));
-    // the next step's tokens, loaded after the far sources: a wait for a far source need not wait for them
-    const uint32_t n0 = tk[tp2 + 4 * lane], n1 = tk[tp2 + 4 * lane + 1], n2 = tk[tp2 + 4 * lane + 2],
-                   n3 = tk[tp2 + 4 * lane + 3], nn = tk[tp2 + 4 * lane + 4];
-    const uint64_t farA = __ballot(mtA && mA.far), farB = __ballot(mtB && mB.far);
-    uint64_t pA = __ballot(mtA), pB = __ballot(mtB);
-    const int endA = mA.mO + mA.Le, endB = mB.mO + mB.Le;
-    while (pA | pB) {
-      // the first pending match in (lane, slot) order
-      const uint64_t pany = pA | pB;
-      const int f = __ffsll((unsigned long long)pany) - 1;
-      const bool fA = (pA >> f) & 1ull;
-      const int fr = fA ? __builtin_amdgcn_readlane(mA.mO, f) : __builtin_amdgcn_readlane(mB.mO, f);
-      const bool ffar = fA ? ((farA >> f) & 1ull) : ((farB >> f) & 1ull);
-      // nearest pending match of the lanes below: the last pending slot of the highest such lane
-      const bool myA = (pA >> lane) & 1ull, myB = (pB >> lane) & 1ull;
-      const uint64_t pb = pany & below;
-      const int jn = pb ? 63 - __clzll((long long)pb) : lane;
-      const int lastEnd = myB ? endB : endA;
-      const int endj = __shfl(lastEnd, jn);
-      const bool rA = mA.srcEnd <= fr || pb == 0 || endj <= mA.mO - mA.d;
-      const bool rB = mB.srcEnd <= fr || (myA ? endA <= mB.mO - mB.d : (pb == 0 || endj <= mB.mO - mB.d));
-      uint64_t readyA = pA & __ballot(rA), readyB = pB & __ballot(rB);
-      if (SBAM_FAR_DEFER && !ffar) {
-        readyA &= ~farA;
-        readyB &= ~farB;
-      }
-      bool gA = (readyA >> lane) & 1ull, gB = (readyB >> lane) & 1ull;
-      while (gA || gB) {  // a lane with both slots ready copies A, then B
-        const rs4::Match m = gA ? mA : mB;
-        const u32x4 pf = gA ? pfA : pfB;
-        int done = 0, deff = m.d;
-        while (done < m.Le) {
-          const int n = min(min(m.Le - done, 16), deff);
-          const int src = m.mO + done - deff;
-          uint32_t v0, v1, v2, v3;
-          if (m.far) {  // below the flushed mark: unaligned 16-B loads, past this CU's L1 (nt)
-            u32x4 x = pf;
-            if (done >= 16) x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(ob + src));
-            v0 = x.x; v1 = x.y; v2 = x.z; v3 = x.w;
-          } else {
-            const uint32_t xs = (Gr + (uint32_t)src) & G::kMask, qs = xs >> 2, ss = xs & 3u;
-            const uint32_t *p = ring + qs;  // (qs + 4 < kDw + kMirror: the mirror covers the wrap)
-            const uint32_t s0 = p[0], s1 = p[1], s2 = p[2], s3 = p[3], s4 = p[4];
-            v0 = __builtin_amdgcn_alignbyte(s1, s0, ss);
-            v1 = __builtin_amdgcn_alignbyte(s2, s1, ss);
-            v2 = __builtin_amdgcn_alignbyte(s3, s2, ss);
-            v3 = __builtin_amdgcn_alignbyte(s4, s3, ss);
-          }
-          const uint4 km = *reinterpret_cast<const uint4 *>(s_keep + 4 * n);  // keep the first n bytes
-          v0 &= km.x;
-          v1 &= km.y;
-          v2 &= km.z;
-          v3 &= km.w;
-          const uint32_t xd = (Gr + (uint32_t)(m.mO + done)) & G::kMask, qd = xd >> 2, s8 = (xd & 3u) * 8u;
-          const uint64_t a01 = ((uint64_t)v1 << 32 | v0) << s8, a12 = ((uint64_t)v2 << 32 | v1) << s8,
-                         a23 = ((uint64_t)v3 << 32 | v2) << s8, a34 = (uint64_t)v3 << s8;
-          ring_or5<G>(ring, qd, (uint32_t)a01, (uint32_t)(a01 >> 32), (uint32_t)(a12 >> 32), (uint32_t)(a23 >> 32),
-                      (uint32_t)(a34 >> 32));
-          done += n;
-          if (n == deff && deff < 16) deff *= 2;  // the copied bytes extend the period: 2·deff is a valid distance
-        }
-        if (gA) gA = false;
-        else gB = false;
-      }
-      pA &= ~readyA;
-      pB &= ~readyB;
-    }
-    // ---- 4. output
-    B = E;
-    if (!head && B >= F0) {  // the block's first partial 16-B chunk (shared with the previous block)
-      if (lane < F0) ob[lane] = ring8[(Gr + (uint32_t)lane) & G::kMask];
-      head = true;
-    }
-    while (B - F >= rs::kFlush) {
-      const uint32_t x = (Gr + (uint32_t)(F + 16 * lane)) & G::kMask;  // 16-B aligned
-      *reinterpret_cast<uint4 *>(ob + F + 16 * lane) = *reinterpret_cast<const uint4 *>(ring8 + x);
-      F += rs::kFlush;
-    }
-    t0 = n0;
-    t1 = n1;
-    t2 = n2;
-    t3 = n3;
-    tn = nn;
-    tp = tp2;
-  }
-  // tail: the head (a block shorter than its first partial chunk), whole 16-B chunks, the last partial chunk
-  if (!head) {
-    if (lane < min(F0, ae)) ob[lane] = ring8[(Gr + (uint32_t)lane) & G::kMask];
-  }
-  if (ae > F0) {
-    const int Ft = F + ((ae - F) & ~15);
-    for (int p = F + 16 * lane; p < Ft; p += rs::kFlush)
-      *reinterpret_cast<uint4 *>(ob + p) = *reinterpret_cast<const uint4 *>(ring8 + ((Gr + (uint32_t)p) & G::kMask));
-    if (Ft + lane < ae) ob[Ft + lane] = ring8[(Gr + (uint32_t)(Ft + lane)) & G::kMask];
-  }
+  if (__ballot(toofar) != 0 && lane == 0 && redo) redo[atomicAdd(nredo, 1u)] = (int32_t)b;
 }
 
 __global__ void k_first_error(const int32_t *__restrict__ status, int64_t n, unsigned long long *first_err) {
@@ -2085,7 +1937,7 @@ hipError_t launch_first_error(const int32_t *status, int64_t n, unsigned long lo
 }
 
 
-hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *tok, int32_t *status,
+hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, TokPool tok, int32_t *status,
                                  int32_t *found, int32_t *slow, unsigned int *counters, hipStream_t s) {
   // counters: [0] slow-path blocks, [1] slow-path work (zeroed first: the host reads [0] back even for 0 blocks)
   (void)hipMemsetAsync(counters, 0, 3 * sizeof(unsigned int), s);
@@ -2097,15 +1949,22 @@ hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, uin
   return hipGetLastError();
 }
 
-hipError_t launch_inflate_resolve(BlockTable bt, uint8_t *out, const uint8_t *tok, const int32_t *found,
+hipError_t launch_inflate_resolve(BlockTable bt, uint8_t *out, TokPool tok, const int32_t *found,
+                                  const int32_t *list, int64_t nlist, int32_t *redo, unsigned int *nredo,
                                   hipStream_t s) {
-  if (bt.n == 0) return hipSuccess;
+  const int64_t n = list ? nlist : bt.n;
+  if (n == 0) return hipSuccess;
   // a 4 KiB ring: 8 waves per SIMD (an 8 KiB ring, 5 per SIMD: 58 ms at 10 GB; 4 KiB: 46 ms)
-#if SBAM_RESOLVE4
-  hipLaunchKernelGGL(k_inflate_resolve4<12>, dim3((unsigned)bt.n), dim3(64), 0, s, bt, out, tok, found);
-#else
-  hipLaunchKernelGGL(k_inflate_resolve<12>, dim3((unsigned)bt.n), dim3(64), 0, s, bt, out, tok, found);
-#endif
+  hipLaunchKernelGGL(k_inflate_resolve<12>, dim3((unsigned)n), dim3(64), 0, s, bt, out, tok, found, list, redo, nredo);
+  return hipGetLastError();
+}
+
+hipError_t launch_inflate_redo(const uint8_t *d, int64_t D, BlockTable bt, TokPool tok, const int32_t *list,
+                               unsigned int *counters, int32_t *status, int32_t *found, hipStream_t s) {
+  // counters[2]: the blocks in list; counters[1]: the exact decoder's work counter, reset
+  (void)hipMemsetAsync(counters + 1, 0, sizeof(unsigned int), s);
+  hipLaunchKernelGGL(k_inflate_slow, dim3(256), dim3(kDecThreads), 0, s, d, D, bt, tok, list, counters + 2, status,
+                     found, counters + 1);
   return hipGetLastError();
 }
 

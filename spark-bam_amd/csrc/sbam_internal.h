@@ -26,6 +26,19 @@ struct BlockTable {
   int64_t n;
 };
 
+// The decode -> resolve token pool.  Block b's u16 tokens live in its main region (1 B per uncompressed byte,
+// tok_region in sbam_inflate.hip: room for (usize + 16) / 2 tokens) unless base[b] >= 0: then at arena + base[b],
+// a region of 2 usize + 32 B taken from the arena by a block that needs more (the exact decoder's blocks, and
+// blocks whose wave decode outgrows the main region: they move there).  arena_used counts every request, also
+// those past arena_cap (the block then reports INF_OVERFLOW and the host grows the arena and inflates again).
+struct TokPool {
+  uint8_t *main;
+  uint8_t *arena;
+  int64_t arena_cap;
+  unsigned long long *arena_used;
+  int64_t *base;
+};
+
 // Stream under check: uncompressed bytes u[0, L) (+ zero pad), contig lengths, EOF semantics.
 struct StreamView {
   const uint8_t *u;
@@ -77,13 +90,20 @@ hipError_t launch_gather_blocks(const Candidate *cands, int64_t first, int64_t n
 // exact path for the blocks it hands over), then LZ77 resolve into `out`.  tok: inflate_token_bytes(L, nb) bytes;
 // slow: nb int32; counters: 3 × u32 device scratch, reset by the decode launch.
 inline size_t inflate_token_bytes(int64_t L, int64_t nb) {
-  // (+1 KiB: the resolver reads up to 4 x 64 + 1 tokens past a step's start)
-  return ((2 * (size_t)L + 15) & ~(size_t)15) + 32 * (size_t)nb + 1024;
+  // main regions (+1 KiB: the resolver reads up to 2 x 64 + 1 tokens past a step's start)
+  return (((size_t)L + 15) & ~(size_t)15) + 32 * (size_t)nb + 1024;
 }
-hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, uint8_t *tok, int32_t *status,
+// default arena: 1/16 of the uncompressed bytes (the synthetic BAM needs none; stored blocks need 2 B per byte)
+inline size_t inflate_arena_bytes(int64_t L) { return (size_t)L / 16 + (1u << 20); }
+hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, TokPool tok, int32_t *status,
                                  int32_t *found, int32_t *slow, unsigned int *counters, hipStream_t s);
-hipError_t launch_inflate_resolve(BlockTable bt, uint8_t *out, const uint8_t *tok, const int32_t *found,
+// list (nlist blocks) or every block; blocks with a distance past their first byte are appended to redo[*nredo]
+hipError_t launch_inflate_resolve(BlockTable bt, uint8_t *out, TokPool tok, const int32_t *found,
+                                  const int32_t *list, int64_t nlist, int32_t *redo, unsigned int *nredo,
                                   hipStream_t s);
+// the exact decoder over list[0 .. counters[2]) (the resolver's redo list)
+hipError_t launch_inflate_redo(const uint8_t *d, int64_t D, BlockTable bt, TokPool tok, const int32_t *list,
+                               unsigned int *counters, int32_t *status, int32_t *found, hipStream_t s);
 // first_err = min block index with status != 0 (caller presets ~0)
 hipError_t launch_first_error(const int32_t *status, int64_t n, unsigned long long *first_err, hipStream_t s);
 hipError_t launch_lower_bound(const Candidate *c, int64_t n, int64_t q, int64_t *out, hipStream_t s);

@@ -260,7 +260,10 @@ def gather_results(res: ShardResult, plans: Sequence[ShardPlan], device=None) ->
 # stream (r per byte, r = uncompressed / compressed), the decoder's token regions (2 r: u16 per uncompressed byte,
 # reserved whole), the success bitmap (r / 8), plus block tables, candidates and the checker's lists (< 0.05).
 def hbm_bytes_per_compressed_byte(ratio: float) -> float:
-    return 1.0 + ratio * (1.0 + 2.0 + 0.125) + 0.05
+    """Device bytes a loaded range needs per compressed byte at compression ratio `ratio`: the compressed bytes, and
+    per uncompressed byte the stream (1), the main token regions (1), the success bitmap (1/8) and the default token
+    arena (1/16); block tables and scratch ~0.05."""
+    return 1.0 + ratio * (1.0 + 1.0 + 0.125 + 0.0625) + 0.05
 
 
 def bgzf_ratio(source: Callable[..., np.ndarray], size: int, sample: int = 8 << 20) -> float:

@@ -300,7 +300,7 @@ def test_hbm_budget_and_auto_windows():
     assert 2.9 < r < 3.2
     assert abs(sdist.bgzf_ratio(lambda lo, hi: src(lo + 1000, hi + 1000), size - 1000) - r) < 0.05
     per = sdist.hbm_bytes_per_compressed_byte(1.1 * r)
-    assert abs(per - (1 + 1.1 * r * 3.125 + 0.05)) < 1e-9
+    assert abs(per - (1 + 1.1 * r * 2.1875 + 0.05)) < 1e-9
     need = size * per * 2
     assert sdist.auto_windows(size, src, int(need / 0.8) + 1) == 1
     assert sdist.auto_windows(size, src, int(need / 0.8 / 3) + 1) == 3

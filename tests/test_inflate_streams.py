@@ -249,3 +249,29 @@ def test_oracle_straddle_distance():
 def test_inflate_round_boundary_distance(distance_ok):
     data = straddle_file(distance_ok)
     assert gpu_result(data) == oracle_result(data)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["stored", "huffman_only"])
+def test_token_arena_growth(kind):
+    """Blocks whose tokens outgrow the main token regions (1 B per output byte): stored blocks (the exact decoder,
+    which always writes into the arena) and Huffman-only blocks (1 token = 2 B per byte: the wave decoder moves them
+    into the arena).  32 MiB of them exceed the default arena (1/16 of the output + 1 MiB), so the first inflate
+    overflows and the host grows the arena and inflates again; the bytes equal zlib's either way."""
+    import sbam
+    r = np.random.default_rng(11)
+    n, size = 512, 65498
+    if kind == "stored":
+        datas = [r.integers(0, 256, size, dtype=np.uint8).tobytes() for _ in range(n)]
+        pays = [deflate(x, 0) for x in datas]
+    else:
+        datas = [r.integers(0, 16, size, dtype=np.uint8).tobytes() for _ in range(n)]
+        pays = [deflate(x, 6, zlib.Z_HUFFMAN_ONLY) for x in datas]
+    data = b"".join(bgzf_block(p, len(x)) for p, x in zip(pays, datas)) + EOF_BLOCK
+    assert gpu_result(data) == ("ok", b"".join(datas))
+    g = sbam.BamFile(data, inflate=False)
+    try:
+        g.inflate()
+        assert g.inflate_fallbacks() == (n if kind == "stored" else 0)
+    finally:
+        g.close()
