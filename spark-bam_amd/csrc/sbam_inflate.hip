@@ -772,6 +772,9 @@ constexpr int kWarm = SBAM_WARM;
 // common case after the warm-up) then only stores them in phase C; it decodes again only past step kTR.  With the
 // round-3 v2 step (38 VALU instead of 58) the register budget is what limits kTR: 96 tokens spilled 48 VGPRs to
 // scratch, 80 spill 11 (decode at 10 GB: 96 → 47.7 ms, 80 → 45.9; 72: 47.5, its phase C re-decodes more tails).
+#ifndef SBAM_CDUMP  // register tokens stored through LDS as whole 16-B chunks (1) or per lane (0)
+#define SBAM_CDUMP 0
+#endif
 #ifndef SBAM_WPRE  // next-window prefetch into registers (WinPre): 1 during phase C, 2 during the table build
 #define SBAM_WPRE 0
 #endif
@@ -1570,7 +1573,8 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       // registers do not hold: mode F its whole segment, mode R the stretch up to its rejoin checkpoint; then the
       // register tokens; then whatever lies past step kTR.
       bool tail = false;
-      uint32_t tail_ti = 0;
+      uint32_t tail_ti = 0, tail_st = 0;
+      uint32_t r_lo = 0, r_hi = 0, r_tb = 0;  // register tokens k in [r_lo, r_hi) go to token index r_tb + k
       if (act) {
         uint32_t start = __shfl_up(nxt, 1);
         if (lane == 0) start = S;
@@ -1597,7 +1601,10 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         const uint32_t n = mode == kModeA ? res.tok : mode == kModeR ? res.tok - rjtk : 0u;
         const uint32_t hi = mode == kModeF ? 0u : min(lo + n, (uint32_t)kTR);
         const uint32_t tb = ti - lo;
-        {
+        r_lo = lo;
+        r_hi = hi;
+        r_tb = tb;
+        if (!SBAM_CDUMP) {
           // 16-B stores (4-B aligned: a 2-B head when tb is odd), dwords and 2-B halves where the run starts or ends
           // inside a chunk — a lane's run is contiguous, so 8 tokens per store instruction instead of one (every
           // store instruction writes 64 lanes' separate lines)
@@ -1635,15 +1642,18 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         }
         WMARK(26);
         WMARK(27);
-        tail = mode != kModeF && lo + n > (uint32_t)kTR;  // the path goes on past step kTR (no stop before it)
-        ti = tb + kTR;
-        tail_ti = ti;
+        // the path goes on past step kTR (no stop before it): phase A's path from step kTR (its state stR) — or, for
+        // a lane that rejoined phase A only after step kTR (no register token is on its path), from the rejoin
+        // checkpoint itself (a literal/length boundary, no pending length) right after the re-decoded stretch
+        tail = mode != kModeF && lo + n > (uint32_t)kTR;
+        tail_st = lo <= (uint32_t)kTR ? stR : rjP << 10;
+        tail_ti = lo <= (uint32_t)kTR ? tb + kTR : ti;
       }
       // the register tokens are stored: their VGPRs take the next window's loads, which the tail decode hides
       if (SBAM_WPRE & 1) pre.fetch(base, base_dw, next_wq, lim_dw);
       if (tail) {
-        uint32_t st4 = (stR >> 7) & 4u, ti = tail_ti;
-        int rp = (int)(stR >> 10);
+        uint32_t st4 = (tail_st >> 7) & 4u, ti = tail_ti;
+        int rp = (int)(tail_st >> 10);
         while (rp < seg_end) {
           uint32_t v;
           const uint32_t kind = wsym(wp, L, rp, st4, v);
@@ -1653,6 +1663,86 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
           ti++;
         }
       }
+#if !SBAM_CDUMP
+      (void)r_lo;
+      (void)r_hi;
+      (void)r_tb;
+#else
+      // the register tokens leave through LDS: staged in the (now free) window 2048 tokens at a time, then stored as
+      // whole, 16-B aligned chunks by consecutive lanes (64 lanes x 16 B contiguous per store instruction instead of
+      // 64 lanes' separate runs); a chunk not entirely made of staged tokens (the round's edges, re-decoded
+      // stretches, which were stored directly) is stored token by token
+      {
+        __syncthreads();  // every lane's decodes are done with the window
+        uint16_t *stg = reinterpret_cast<uint16_t *>(L.win);  // [2048]
+        uint32_t *vld = L.win + 1024;                          // [64]: bit t = token P0 + t staged
+        const int T0 = ntok & ~7, T1 = ntok + (int)tot_tok;
+        const uint32_t par = r_tb & 1u;
+        auto dw = [&](auto Q) {  // register dword q: tokens k = par + 2q, par + 2q + 1
+          constexpr int q = decltype(Q)::value;
+          const uint32_t nx = q + 1 < kTR / 2 ? tr[q + 1 < kTR / 2 ? q + 1 : q] : 0u;
+          return par ? __builtin_amdgcn_alignbit(nx, tr[q], 16) : tr[q];
+        };
+        for (int P0 = T0; P0 < T1; P0 += 2048) {
+          vld[lane] = 0u;
+          __syncthreads();
+          const int ka = max((int)r_lo, P0 - (int)r_tb), kb = min((int)r_hi, P0 + 2048 - (int)r_tb);
+          if (ka < kb) {
+            // staging dword of register dword q: (r_tb + par + 2q - P0) / 2 = sd0 + q
+            const int sd0 = ((int)r_tb + (int)par - P0) >> 1;
+            uint32_t *sw = reinterpret_cast<uint32_t *>(stg);
+            if (par && ka == 0) stg[r_tb - P0] = (uint16_t)tr[0];  // token 0 alone in the high half of its dword
+            sfor<0, kTR / 8>([&](auto C) {
+              constexpr int c = decltype(C)::value;
+              const int t0 = (int)par + 8 * c;
+              if (t0 + 8 > ka && t0 < kb) {
+                const uint32_t a0 = dw(std::integral_constant<int, 4 * c>{}), a1 = dw(std::integral_constant<int, 4 * c + 1>{});
+                const uint32_t a2 = dw(std::integral_constant<int, 4 * c + 2>{}), a3 = dw(std::integral_constant<int, 4 * c + 3>{});
+                if (t0 >= ka && t0 + 8 <= kb) {
+                  sw[sd0 + 4 * c] = a0;
+                  sw[sd0 + 4 * c + 1] = a1;
+                  sw[sd0 + 4 * c + 2] = a2;
+                  sw[sd0 + 4 * c + 3] = a3;
+                } else {
+                  const uint32_t a[4] = {a0, a1, a2, a3};
+#pragma unroll
+                  for (int k = 0; k < 4; k++) {
+                    const int u0 = t0 + 2 * k;
+                    const bool in0 = u0 >= ka && u0 < kb, in1 = u0 + 1 >= ka && u0 + 1 < kb;
+                    uint16_t *ph = reinterpret_cast<uint16_t *>(sw + sd0 + 4 * c + k);
+                    if (in0 && in1) sw[sd0 + 4 * c + k] = a[k];
+                    else if (in0) ph[0] = (uint16_t)a[k];
+                    else if (in1) ph[1] = (uint16_t)(a[k] >> 16);
+                  }
+                }
+              }
+            });
+            // staged flags of tokens [r_tb + ka - P0, r_tb + kb - P0)
+            const int fa = (int)r_tb + ka - P0, fb = (int)r_tb + kb - P0;
+            for (int w = fa >> 5; w <= (fb - 1) >> 5; w++) {
+              const int lo32 = max(fa - 32 * w, 0), hi32 = min(fb - 32 * w, 32);
+              const uint32_t m = (hi32 >= 32 ? ~0u : (1u << hi32) - 1u) & ~((1u << lo32) - 1u);
+              atomicOr(vld + w, m);
+            }
+          }
+          __syncthreads();
+#pragma unroll
+          for (int i = 0; i < 4; i++) {
+            const int j = lane + 64 * i, t = P0 + 8 * j;
+            if (t < T1) {
+              const uint32_t m = (vld[j >> 2] >> (8 * (j & 3))) & 0xffu;
+              if (m == 0xffu) {
+                *reinterpret_cast<uint4 *>(reg + 2 * (int64_t)t) = *reinterpret_cast<const uint4 *>(stg + 8 * j);
+              } else if (m) {
+                for (int k = 0; k < 8; k++)
+                  if ((m >> k) & 1u) reinterpret_cast<uint16_t *>(reg)[t + k] = stg[8 * j + k];
+              }
+            }
+          }
+          __syncthreads();
+        }
+      }
+#endif
       WMARK(28);
       out += (int)tot_byt;
       ntok += (int)tot_tok;

@@ -2,6 +2,7 @@
 // layer (sbam_api.cpp).  Not part of the public ABI (include/sbam.h is).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <stdint.h>
 
 namespace sbam {
@@ -94,7 +95,12 @@ inline size_t inflate_token_bytes(int64_t L, int64_t nb) {
   return (((size_t)L + 15) & ~(size_t)15) + 32 * (size_t)nb + 1024;
 }
 // default arena: 1/16 of the uncompressed bytes (the synthetic BAM needs none; stored blocks need 2 B per byte)
-inline size_t inflate_arena_bytes(int64_t L) { return (size_t)L / 16 + (1u << 20); }
+// (SBAM_ARENA_MB overrides it: tests of the arena's growth)
+inline size_t inflate_arena_bytes(int64_t L) {
+  const char *e = std::getenv("SBAM_ARENA_MB");
+  if (e && *e) return (size_t)std::atoll(e) << 20;
+  return (size_t)L / 16 + (1u << 20);
+}
 hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, TokPool tok, int32_t *status,
                                  int32_t *found, int32_t *slow, unsigned int *counters, hipStream_t s);
 // list (nlist blocks) or every block; blocks with a distance past their first byte are appended to redo[*nredo]

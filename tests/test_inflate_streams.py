@@ -252,8 +252,9 @@ def test_inflate_round_boundary_distance(distance_ok):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("arena_mb", ["", "256"])
 @pytest.mark.parametrize("kind", ["stored", "huffman_only"])
-def test_token_arena_growth(kind):
+def test_token_arena_growth(kind, arena_mb, monkeypatch):
     """Blocks whose tokens outgrow the main token regions (1 B per output byte): stored blocks (the exact decoder,
     which always writes into the arena) and Huffman-only blocks (1 token = 2 B per byte: the wave decoder moves them
     into the arena).  32 MiB of them exceed the default arena (1/16 of the output + 1 MiB), so the first inflate
@@ -268,7 +269,11 @@ def test_token_arena_growth(kind):
         datas = [r.integers(0, 16, size, dtype=np.uint8).tobytes() for _ in range(n)]
         pays = [deflate(x, 6, zlib.Z_HUFFMAN_ONLY) for x in datas]
     data = b"".join(bgzf_block(p, len(x)) for p, x in zip(pays, datas)) + EOF_BLOCK
-    assert gpu_result(data) == ("ok", b"".join(datas))
+    monkeypatch.setenv("SBAM_ARENA_MB", arena_mb)  # "" = the default (1/16 of the output: grown once)
+    kind_, out = gpu_result(data)
+    assert kind_ == "ok"
+    bad = [i for i in range(n) if out[i * size:(i + 1) * size] != datas[i]]
+    assert not bad, (len(bad), bad[:8], len(out))
     g = sbam.BamFile(data, inflate=False)
     try:
         g.inflate()
