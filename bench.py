@@ -304,8 +304,10 @@ def main():
     res = None
     for _ in range(args.warmup):
         res, _ = step()
-    if pipe is not None:  # the first timed step loads its window 0 itself (no prefetch from the warm-up)
-        pipe.drop_prefetch()
+    # a streamed pipe runs on from the warm-up into the timed steps (steady state: every step loads W windows — its
+    # windows 1..W-1 and the next step's window 0 — and the first timed step's window 0 was loaded during the
+    # warm-up's last window); round 3 dropped that prefetch, so the first timed step loaded its window 0 in the
+    # foreground (a step ~200 ms longer than the rest at 30 GB / 3 windows)
     tot_ms = {k: 0.0 for k in kernels}
     sync()
     t0 = time.perf_counter()
@@ -382,8 +384,7 @@ def main():
 
         epipe = sdist.WindowPipe(wplans_of(args.e2e_windows), stage_pinned, split_size, s.contig_lengths, local,
                                  run_window, prefetch=True)
-        merge(epipe.step())  # warm-up (allocations)
-        epipe.drop_prefetch()  # the first timed step loads its window 0 in the foreground
+        merge(epipe.step())  # warm-up (allocations); the pipe runs on into the timed steps (steady state)
         sync()
         t1 = time.perf_counter()
         for _ in range(args.e2e_steps):
@@ -391,13 +392,14 @@ def main():
         sync()
         e_el = max_over_ranks(time.perf_counter() - t1)
         e_ok = sdist.unpack_counts(eres.counts)["n_success"] == int(eres.n_records.sum())
+        epipe.drop_prefetch()
         epipe.close()
         e2e = {"value": round(s.size * args.e2e_steps / e_el / 1e9, 3), "unit": "GB/s",
                "ms_per_step": round(e_el / args.e2e_steps * 1e3, 3), "windows": args.e2e_windows,
                "steps": args.e2e_steps, "parity_ok": bool(e_ok),
                "how": "compressed bytes in pinned host memory, streamed in windows through two contexts: window "
                       "w+1's H2D (sbam_load) overlaps window w's kernels, and a step's last window overlaps the next "
-                      "step's window 0 (the first timed step loads its window 0 in the foreground)"}
+                      "step's window 0 (steady state: the pipe runs on from the warm-up step)"}
         del host
 
     if rank == 0:
@@ -468,6 +470,7 @@ def main():
     if shard is not None:
         shard.close()
     if pipe is not None:
+        pipe.drop_prefetch()
         pipe.close()
     if world > 1:
         dist.destroy_process_group()

@@ -396,6 +396,9 @@ int sbam_reserve(sbam_ctx *c, int64_t comp_bytes, int64_t n_blocks, int64_t ubyt
     HIPCHK(c, ensure(&c->d_pfb, &c->pfb_cap, n));
     HIPCHK(c, ensure(&c->d_pok, &c->pok_cap, n));
     HIPCHK(c, ensure(&c->d_roff, &c->roff_cap, n));
+    // loadReads' columns (sbam_load_records: an int64 column and ten int32 ones, 256-B aligned)
+    const size_t stride = (n * 8 + 255) & ~(size_t)255, stride4 = (n * 4 + 255) & ~(size_t)255;
+    HIPCHK(c, ensure(&c->d_rcols, &c->rcols_cap, stride + 10 * stride4));
   }
   return SBAM_OK;
 }
