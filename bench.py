@@ -96,20 +96,22 @@ def copy_peak(dev) -> dict:
     grid-stride) over 4 GiB device to device, read + write bytes / kernel time; the best of a few grid sizes."""
     import ctypes
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "build", "libhbmpeak.so"))
-    lib.hbm_copy_peak.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+    lib.hbm_copy_peak.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                   ctypes.POINTER(ctypes.c_double)]
     n = 4 << 30
     best = None
-    for grid in (1024, 2048, 4096, 8192):
-        ms = ctypes.c_double(0.0)
-        rc = lib.hbm_copy_peak(dev.index or 0, n, 10, grid, ctypes.byref(ms))
-        if rc == 0 and ms.value > 0 and (best is None or ms.value < best[1]):
-            best = (grid, ms.value)
+    for nt in (0, 1):
+        for grid in (2048, 8192, 32768):
+            ms = ctypes.c_double(0.0)
+            rc = lib.hbm_copy_peak(dev.index or 0, n, 10, grid, nt, ctypes.byref(ms))
+            if rc == 0 and ms.value > 0 and (best is None or ms.value < best[2]):
+                best = (grid, nt, ms.value)
     if best is None:
         raise RuntimeError("hbm_copy_peak failed")
-    return {"value": round(2 * n / (best[1] * 1e-3) / 1e9, 1), "unit": "GB/s", "bytes": 2 * n,
-            "how": f"tools/hbm_peak.hip: global_load/store_dwordx4 (nontemporal) copy of 4 GiB device->device, "
-                   f"read+write bytes / kernel time, 10 reps, best grid {best[0]} x 256"}
+    return {"value": round(2 * n / (best[2] * 1e-3) / 1e9, 1), "unit": "GB/s", "bytes": 2 * n,
+            "how": f"tools/hbm_peak.hip: global_load/store_dwordx4 copy of 4 GiB device->device "
+                   f"({'nontemporal' if best[1] else 'plain'}), read+write bytes / kernel time, 10 reps, "
+                   f"best of grids 2048/8192/32768 x 256 and plain/nontemporal: {best[0]}"}
 
 
 def cpu_baseline(sample_mb: float, threads: int, split_size: int, seed: int, tiles: int = 1):

@@ -1188,9 +1188,11 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bi
         const int32_t lrn = (int32_t)((W[3] >> (8 * o)) & 0xffu);
         const int32_t nc = (int32_t)(fld(4) & 0xffffu);
         const int32_t ls = (int32_t)fld(5);
-        const uint32_t last = s_win[rel + 35 + lrn];  // the name's last byte (read for lrn < 2 too, unused then)
-        // first invalid op (>= 64: none among the first 64); ops start at 36 + lrn, or 36 when lrn < 2: lrn = 0
-        // reads the right byte, lrn = 1 is redone below
+        // the name's last byte (read for lrn < 2 too, unused then); first invalid op (>= 64: none among the first
+        // 64); ops start at 36 + lrn, or 36 when lrn < 2: lrn = 0 reads the right byte, lrn = 1 is redone below.
+        // (Round 4: both bits from one fb byte — bit 7 = "byte before is 0", set in stage_fb — was slower, 43.2 vs
+        // 41.4 ms: the stage_fb work costs more than the LDS read it saves.)
+        const uint32_t last = s_win[rel + 35 + lrn];
         const uint32_t obad = s_fb[rel + 36 + lrn];
         pLZ = push_bit(pLZ, last == 0);
         pIV = push_bit(pIV, obad < min((uint32_t)nc, 64u));  // an invalid op among the first min(nc, 64)

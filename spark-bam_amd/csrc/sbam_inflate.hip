@@ -783,6 +783,7 @@ constexpr int kWarm = SBAM_WARM;
 #endif
 constexpr int kTR = SBAM_TR;
 static_assert(kTR % 2 == 0 && kTR <= kCp * kCpSteps, "register tokens come from the unrolled checkpoint steps");
+static_assert(kTR % kCpSteps == 0, "the state after step kTR (stR) is saved at a checkpoint");
 constexpr int kScratchDw = 256;    // window tail that doubles as header / table-build scratch
 // a block header (<= 3 + 14 + 57 + 320 * 14 bits) plus the window's start alignment fits before the scratch
 static_assert(128 + 3 + 14 + 57 + 320 * 14 + 64 <= (kWinDw - kScratchDw) * 32, "header fits the window");
