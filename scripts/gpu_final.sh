@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/final
 mkdir -p $OUT
 if [ "${PART:-1}" = 1 ]; then
-  timeout -k 10 500 python -u -m pytest tests/ -q -m gpu --timeout 200 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || exit 1
+  timeout -k 10 900 python -u -m pytest tests/ -q -m gpu --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || exit 1
   timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit 2
   timeout -k 10 400 python -u bench.py > $OUT/bench_default.log 2>&1 || exit 3
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_bench -o p -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --e2e-windows 0 > $OUT/bench_prof.log 2>&1 || exit 4
