@@ -31,7 +31,8 @@
 #define SBAM_CHECK_WGS_INT 5
 #endif
 #ifndef SBAM_CHECK_WGS_BITS
-#define SBAM_CHECK_WGS_BITS 5  // k_check_bits (6 spills a few constants: +7 GB scratch traffic, same time)
+#define SBAM_CHECK_WGS_BITS 5  // k_check_bits (6 spills a few constants: +7 GB scratch traffic, same time; round 4 with
+                               // the LDS trimmed to 26.8 KB so that 6 workgroups fit: 41.5 vs 41.2 ms — not latency-bound)
 #endif
 #ifndef SBAM_LDS_LENS
 #define SBAM_LDS_LENS 4096

@@ -782,6 +782,9 @@ constexpr int kWarm = SBAM_WARM;
 #define SBAM_TR 80
 #endif
 constexpr int kTR = SBAM_TR;
+#ifndef SBAM_TR_PIN  // register tokens forced into VGPRs before phase C's stores: 1 before the re-decode, 2 after it
+#define SBAM_TR_PIN 2
+#endif
 static_assert(kTR % 2 == 0 && kTR <= kCp * kCpSteps, "register tokens come from the unrolled checkpoint steps");
 static_assert(kTR % kCpSteps == 0, "the state after step kTR (stR) is saved at a checkpoint");
 constexpr int kScratchDw = 256;    // window tail that doubles as header / table-build scratch
@@ -1576,6 +1579,12 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       bool tail = false;
       uint32_t tail_ti = 0, tail_st = 0;
       uint32_t r_lo = 0, r_hi = 0, r_tb = 0;  // register tokens k in [r_lo, r_hi) go to token index r_tb + k
+#if SBAM_TR_PIN == 1
+      // every register token in a VGPR before the first token store: phase A spills a few of them, and a reload
+      // issued after stores waits for all of them (one in-order vmcnt: four store drains per round otherwise)
+      static_assert(kTR == 80, "one asm operand per register token dword");
+      asm volatile("" : "+v"(tr[0]), "+v"(tr[1]), "+v"(tr[2]), "+v"(tr[3]), "+v"(tr[4]), "+v"(tr[5]), "+v"(tr[6]), "+v"(tr[7]), "+v"(tr[8]), "+v"(tr[9]), "+v"(tr[10]), "+v"(tr[11]), "+v"(tr[12]), "+v"(tr[13]), "+v"(tr[14]), "+v"(tr[15]), "+v"(tr[16]), "+v"(tr[17]), "+v"(tr[18]), "+v"(tr[19]), "+v"(tr[20]), "+v"(tr[21]), "+v"(tr[22]), "+v"(tr[23]), "+v"(tr[24]), "+v"(tr[25]), "+v"(tr[26]), "+v"(tr[27]), "+v"(tr[28]), "+v"(tr[29]), "+v"(tr[30]), "+v"(tr[31]), "+v"(tr[32]), "+v"(tr[33]), "+v"(tr[34]), "+v"(tr[35]), "+v"(tr[36]), "+v"(tr[37]), "+v"(tr[38]), "+v"(tr[39]));
+#endif
       if (act) {
         uint32_t start = __shfl_up(nxt, 1);
         if (lane == 0) start = S;
@@ -1605,6 +1614,11 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         r_lo = lo;
         r_hi = hi;
         r_tb = tb;
+#if SBAM_TR_PIN == 2
+        static_assert(kTR == 80, "one asm operand per register token dword");
+        // (one statement: the spilled ones are reloaded together, one wait)
+        asm volatile("" : "+v"(tr[0]), "+v"(tr[1]), "+v"(tr[2]), "+v"(tr[3]), "+v"(tr[4]), "+v"(tr[5]), "+v"(tr[6]), "+v"(tr[7]), "+v"(tr[8]), "+v"(tr[9]), "+v"(tr[10]), "+v"(tr[11]), "+v"(tr[12]), "+v"(tr[13]), "+v"(tr[14]), "+v"(tr[15]), "+v"(tr[16]), "+v"(tr[17]), "+v"(tr[18]), "+v"(tr[19]), "+v"(tr[20]), "+v"(tr[21]), "+v"(tr[22]), "+v"(tr[23]), "+v"(tr[24]), "+v"(tr[25]), "+v"(tr[26]), "+v"(tr[27]), "+v"(tr[28]), "+v"(tr[29]), "+v"(tr[30]), "+v"(tr[31]), "+v"(tr[32]), "+v"(tr[33]), "+v"(tr[34]), "+v"(tr[35]), "+v"(tr[36]), "+v"(tr[37]), "+v"(tr[38]), "+v"(tr[39]));
+#endif
         if (!SBAM_CDUMP) {
           // 16-B stores (4-B aligned: a 2-B head when tb is odd), dwords and 2-B halves where the run starts or ends
           // inside a chunk — a lane's run is contiguous, so 8 tokens per store instruction instead of one (every
@@ -1793,6 +1807,15 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
 #ifndef SBAM_FAR_DEFER
 #define SBAM_FAR_DEFER 0
 #endif
+#ifndef SBAM_RES_FARWAIT
+#define SBAM_RES_FARWAIT 1
+#endif
+#ifndef SBAM_RES_EARLYFLUSH
+#define SBAM_RES_EARLYFLUSH 1
+#endif
+#ifndef SBAM_RES_TOKWAIT
+#define SBAM_RES_TOKWAIT 1
+#endif
 namespace rs {
 constexpr int kSpan = 1024;   // a chunk's words start within kSpan bytes of its base
 constexpr int kFlush = 1024;  // output bytes per group store (64 lanes x 16 B)
@@ -1873,6 +1896,9 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
   bool toofar = false;                            // a distance past the block's first byte (zlib: data error)
   // lane i holds tokens tp + 2i and tp + 2i + 1, and sees tp + 2i + 2 (the distance of a length in its second)
   uint32_t ta = tk[2 * lane], tb = tk[2 * lane + 1], tn = tk[2 * lane + 2];
+#if SBAM_RES_TOKWAIT
+  asm volatile("" : "+v"(ta), "+v"(tb), "+v"(tn));  // (no token load pending at the loop head, from either edge)
+#endif
   while (B < ae) {
     // ---- 1. positions: a lane yields up to 2 literals and at most one match (a length in its first token takes
     // the second as its distance; a length in its second takes the next lane's first)
@@ -1918,6 +1944,20 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
         if (x1 < 4u * G::kMirror) ring8[G::kRing + x1] = (uint8_t)(lv >> 8);
       }
     }
+#if SBAM_RES_EARLYFLUSH
+    // ---- 4. output of the chunks before this one ([F, B) is final), issued before this step's loads: the stores
+    // precede the next step's token loads, so waiting for those never waits for the stores (one in-order vmcnt; a
+    // data-dependent store count after the loads made the compiler wait with vmcnt(0))
+    if (!head && B >= F0) {  // the block's first partial 16-B chunk (shared with the previous block)
+      if (lane < F0) ob[lane] = ring8[(Gr + (uint32_t)lane) & G::kMask];
+      head = true;
+    }
+    while (B - F >= rs::kFlush) {
+      const uint32_t x = (Gr + (uint32_t)(F + 16 * lane)) & G::kMask;  // 16-B aligned
+      *reinterpret_cast<uint4 *>(ob + F + 16 * lane) = *reinterpret_cast<const uint4 *>(ring8 + x);
+      F += rs::kFlush;
+    }
+#endif
     // ---- 3b. matches, in rounds
     const int mO = O + (bLen ? nl : 0);
     int Le = (take && Lm > 0) ? min(Lm, ae - mO) : 0;
@@ -1935,7 +1975,14 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
       if (Le > 16) pf1 = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(ob + mO - d + 16));
     }
     // the next step's tokens, loaded after the far sources: a wait for a far source need not wait for them
+#if SBAM_RES_TOKWAIT
+    // (as raw registers, split only after the rounds: see the end of the step)
+    uint32_t w2, n2;
+    __builtin_memcpy(&w2, tk + tp2 + 2 * lane, 4);
+    n2 = tk[tp2 + 2 * lane + 2];
+#else
     const uint32_t ta2 = tk[tp2 + 2 * lane], tb2 = tk[tp2 + 2 * lane + 1], tn2 = tk[tp2 + 2 * lane + 2];
+#endif
     const uint64_t farm = __ballot(mt && far);
     uint64_t pend = __ballot(mt);
     const uint64_t below = (1ull << lane) - 1ull;
@@ -1957,9 +2004,24 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
           const int src = mO + done - deff;
           uint32_t v0, v1, v2, v3;
           if (far) {  // below the flushed mark: unaligned 16-B loads, past this CU's L1 (nt)
+#if SBAM_RES_FARWAIT
+            // each path waits for its own source here (the prefetched ones: vmcnt(2), the next step's two token
+            // loads may stay in flight): merged with the near path's registers, the compiler waited with vmcnt(0)
+            // after the join, so every near copy also waited for the next step's tokens
+            if (done >= 32) {
+              const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(ob + src));
+              v0 = x.x; v1 = x.y; v2 = x.z; v3 = x.w;
+              asm volatile("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));
+            } else {
+              const u32x4 x = done == 0 ? pf0 : pf1;
+              v0 = x.x; v1 = x.y; v2 = x.z; v3 = x.w;
+              asm volatile("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));
+            }
+#else
             u32x4 x = done == 0 ? pf0 : pf1;
             if (done >= 32) x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(ob + src));
             v0 = x.x; v1 = x.y; v2 = x.z; v3 = x.w;
+#endif
           } else {
             const uint32_t xs = (Gr + (uint32_t)src) & G::kMask, qs = xs >> 2, ss = xs & 3u;
             const uint32_t *p = ring + qs;  // (qs + 4 < kDw + kMirror: the mirror covers the wrap)
@@ -1987,8 +2049,9 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
       }
       pend &= ~ready;
     }
-    // ---- 4. output
     B = E;
+#if !SBAM_RES_EARLYFLUSH
+    // ---- 4. output
     if (!head && B >= F0) {  // the block's first partial 16-B chunk (shared with the previous block)
       if (lane < F0) ob[lane] = ring8[(Gr + (uint32_t)lane) & G::kMask];
       head = true;
@@ -1998,9 +2061,19 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
       *reinterpret_cast<uint4 *>(ob + F + 16 * lane) = *reinterpret_cast<const uint4 *>(ring8 + x);
       F += rs::kFlush;
     }
+#endif
+#if SBAM_RES_TOKWAIT
+    // the wait for the next step's tokens, here: the compiler otherwise split them right after the loads (waiting
+    // there), or let this step's last use of tn wait after the stores (one in-order vmcnt)
+    asm volatile("" : "+v"(w2), "+v"(n2));
+    ta = w2 & 0xffffu;
+    tb = w2 >> 16;
+    tn = n2;
+#else
     ta = ta2;
     tb = tb2;
     tn = tn2;
+#endif
     tp = tp2;
   }
   // tail: the head (a block shorter than its first partial chunk), whole 16-B chunks, the last partial chunk
