@@ -782,6 +782,10 @@ constexpr int kWarm = SBAM_WARM;
 #define SBAM_TR 80
 #endif
 constexpr int kTR = SBAM_TR;
+#ifndef SBAM_STAGE_UNROLL  // window staging: LDS DMA (2), all loads into VGPRs before one wait (1), a load-wait-store
+                           // loop (0); decode at 10 GB 41.07 / 41.46 / 41.93 ms
+#define SBAM_STAGE_UNROLL 2
+#endif
 #ifndef SBAM_TR_PIN  // register tokens forced into VGPRs before phase C's stores: 1 before the re-decode, 2 after it
 #define SBAM_TR_PIN 2
 #endif
@@ -1017,15 +1021,50 @@ struct HBits {
 };
 
 // Stage kWinDw dwords from dword wq_dw of the block's aligned base into the window (zeros past the buffer).
+// Every load is issued before the first wait: as a loop (load, wait, LDS store per 1 KiB) the compiler waited for
+// each load in turn — five memory round trips per round instead of one.
 SB_DEV void wave_stage(uint32_t *win, const uint32_t *base, int64_t base_dw, int wq_dw, int64_t lim_dw) {
+  constexpr int kN = (wd::kWinDw + 255) / 256;
   const int lane = (int)threadIdx.x;
   __syncthreads();  // every lane is done with the previous window
+#if SBAM_STAGE_UNROLL == 2
+  // LDS DMA (global_load_lds_dwordx4: lane l's 16 B land at the LDS base + 16 l), no VGPRs; lanes past the buffer
+  // load its last 16 B instead of zeros (bits past the payload only ever end a speculative path: ST_OUT)
+  {
+    const int64_t last = lim_dw - 4 - base_dw;  // dword offset of the buffer's last 16 B from base
+#pragma unroll
+    for (int k = 0; k < kN; k++) {
+      const int i = lane * 4 + 256 * k;
+      if (i < wd::kWinDw) {  // (exec-masked: lanes past the window write nothing — the tables follow it)
+        int64_t o = (int64_t)wq_dw + i;
+        o = o > last ? last : o;
+        __builtin_amdgcn_global_load_lds(base + o, win + 256 * k, 16, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+#elif SBAM_STAGE_UNROLL
+  uint4 v[kN];
+#pragma unroll
+  for (int k = 0; k < kN; k++) {
+    const int i = lane * 4 + 256 * k;
+    const int64_t g = base_dw + wq_dw + i;
+    v[k] = (i < wd::kWinDw && g + 4 <= lim_dw) ? *reinterpret_cast<const uint4 *>(base + wq_dw + i)
+                                                 : make_uint4(0, 0, 0, 0);
+  }
+#pragma unroll
+  for (int k = 0; k < kN; k++) {
+    const int i = lane * 4 + 256 * k;
+    if (i < wd::kWinDw) *reinterpret_cast<uint4 *>(win + i) = v[k];
+  }
+#else
   for (int i = lane * 4; i < wd::kWinDw; i += 256) {
     const int64_t g = base_dw + wq_dw + i;
     uint4 v = make_uint4(0, 0, 0, 0);
     if (g + 4 <= lim_dw) v = *reinterpret_cast<const uint4 *>(base + wq_dw + i);
     *reinterpret_cast<uint4 *>(win + i) = v;
   }
+#endif
   __syncthreads();
 }
 // The same window loaded into registers ahead of time (WinPre::fetch as soon as the next window's start is known:
@@ -1073,7 +1112,7 @@ struct SegResult {
 };
 
 #ifdef SBAM_WAVE_STATS
-constexpr int kWaveStats = 32;
+constexpr int kWaveStats = 40;  // [0, 32): k_inflate_wave, [32, 40): k_inflate_resolve
 __device__ unsigned long long g_wave_stats[kWaveStats];
 #define WMARK(slot) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); ws_[slot] += t_ - wt_; wt_ = t_; } while (0)
 #define WADD(slot, v) ws_[slot] += (v)
@@ -1088,6 +1127,11 @@ extern "C" int sbam_debug_wave_stats(unsigned long long *out, int reset) {
 #else
 #define WMARK(slot) do {} while (0)
 #define WADD(slot, v) do {} while (0)
+#endif
+#ifdef SBAM_WAVE_STATS  // resolver phases: slot 32 + k (RMARK), 39 = steps
+#define RMARK(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); rs_[k] += t_ - rt_; rt_ = t_; } while (0)
+#else
+#define RMARK(k) do {} while (0)
 #endif
 
 __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restrict__ d, int64_t D, BlockTable bt,
@@ -1121,7 +1165,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
   int out = 0, ntok = 0;
   bool ok = true;
 #ifdef SBAM_WAVE_STATS
-  uint64_t ws_[kWaveStats] = {0};
+  uint64_t ws_[32] = {0};  // (slots 32.. are the resolver's)
   uint64_t wt_ = __builtin_amdgcn_s_memtime();
   const uint64_t wt0_ = wt_;
 #endif
@@ -1619,6 +1663,11 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         // (one statement: the spilled ones are reloaded together, one wait)
         asm volatile("" : "+v"(tr[0]), "+v"(tr[1]), "+v"(tr[2]), "+v"(tr[3]), "+v"(tr[4]), "+v"(tr[5]), "+v"(tr[6]), "+v"(tr[7]), "+v"(tr[8]), "+v"(tr[9]), "+v"(tr[10]), "+v"(tr[11]), "+v"(tr[12]), "+v"(tr[13]), "+v"(tr[14]), "+v"(tr[15]), "+v"(tr[16]), "+v"(tr[17]), "+v"(tr[18]), "+v"(tr[19]), "+v"(tr[20]), "+v"(tr[21]), "+v"(tr[22]), "+v"(tr[23]), "+v"(tr[24]), "+v"(tr[25]), "+v"(tr[26]), "+v"(tr[27]), "+v"(tr[28]), "+v"(tr[29]), "+v"(tr[30]), "+v"(tr[31]), "+v"(tr[32]), "+v"(tr[33]), "+v"(tr[34]), "+v"(tr[35]), "+v"(tr[36]), "+v"(tr[37]), "+v"(tr[38]), "+v"(tr[39]));
 #endif
+#ifndef SBAM_DUMP_REPS  // (diagnostic: the register tokens stored this many times, to price the stores)
+#define SBAM_DUMP_REPS 1
+#endif
+#pragma unroll 1
+        for (int rep_ = 0; rep_ < SBAM_DUMP_REPS; rep_++)
         if (!SBAM_CDUMP) {
           // 16-B stores (4-B aligned: a 2-B head when tb is odd), dwords and 2-B halves where the run starts or ends
           // inside a chunk — a lane's run is contiguous, so 8 tokens per store instruction instead of one (every
@@ -1772,7 +1821,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
 #ifdef SBAM_WAVE_STATS
   ws_[8] = __builtin_amdgcn_s_memtime() - wt0_;
   if (lane == 0)
-    for (int i = 0; i < kWaveStats; i++) atomicAdd(&g_wave_stats[i], (unsigned long long)ws_[i]);
+    for (int i = 0; i < 29; i++) atomicAdd(&g_wave_stats[i], (unsigned long long)ws_[i]);
 #endif
   if (lane == 0) {
     if (ok) {
@@ -1899,6 +1948,13 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
 #if SBAM_RES_TOKWAIT
   asm volatile("" : "+v"(ta), "+v"(tb), "+v"(tn));  // (no token load pending at the loop head, from either edge)
 #endif
+#ifdef SBAM_WAVE_STATS
+  uint64_t rs_[8] = {0};
+  uint32_t it_ = 0;
+  uint64_t itw_ = 0, itl_ = 0;
+  uint64_t rt_ = __builtin_amdgcn_s_memtime();
+  const uint64_t rt0_ = rt_;
+#endif
   while (B < ae) {
     // ---- 1. positions: a lane yields up to 2 literals and at most one match (a length in its first token takes
     // the second as its distance; a length in its second takes the next lane's first)
@@ -1930,6 +1986,7 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
       }
       Z = (int)(z1 * 4u - Gr);
     }
+    RMARK(0);  // positions, ring zeroing
     // ---- 3a. literals (before the match when a lane has both)
     // (byte stores: they touch only their own byte, so lanes writing neighbouring bytes of a dword never race)
     const int Ll = take ? min(nl, ae - O) : 0;
@@ -1944,6 +2001,7 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
         if (x1 < 4u * G::kMirror) ring8[G::kRing + x1] = (uint8_t)(lv >> 8);
       }
     }
+    RMARK(1);  // literals
 #if SBAM_RES_EARLYFLUSH
     // ---- 4. output of the chunks before this one ([F, B) is final), issued before this step's loads: the stores
     // precede the next step's token loads, so waiting for those never waits for the stores (one in-order vmcnt; a
@@ -1958,6 +2016,7 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
       F += rs::kFlush;
     }
 #endif
+    RMARK(2);  // output stores
     // ---- 3b. matches, in rounds
     const int mO = O + (bLen ? nl : 0);
     int Le = (take && Lm > 0) ? min(Lm, ae - mO) : 0;
@@ -1983,6 +2042,7 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
 #else
     const uint32_t ta2 = tk[tp2 + 2 * lane], tb2 = tk[tp2 + 2 * lane + 1], tn2 = tk[tp2 + 2 * lane + 2];
 #endif
+    RMARK(3);  // match setup, far prefetch, next tokens issued
     const uint64_t farm = __ballot(mt && far);
     uint64_t pend = __ballot(mt);
     const uint64_t below = (1ull << lane) - 1ull;
@@ -2000,6 +2060,9 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
       if ((ready >> lane) & 1ull) {
         int done = 0, deff = d;
         while (done < Le) {
+#ifdef SBAM_WAVE_STATS
+          it_++;
+#endif
           const int n = min(min(Le - done, 16), deff);
           const int src = mO + done - deff;
           uint32_t v0, v1, v2, v3;
@@ -2048,7 +2111,21 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
         }
       }
       pend &= ~ready;
+#ifdef SBAM_WAVE_STATS
+      rs_[7]++;  // rounds
+      {  // copy iterations: the wave's (the slowest lane's) and the sum over lanes
+        uint32_t mx = it_, sm = it_;
+        for (int o = 32; o >= 1; o >>= 1) {
+          mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+          sm += (uint32_t)__shfl_xor((int)sm, o);
+        }
+        itw_ += mx;
+        itl_ += sm;
+        it_ = 0;
+      }
+#endif
     }
+    RMARK(4);  // rounds
     B = E;
 #if !SBAM_RES_EARLYFLUSH
     // ---- 4. output
@@ -2069,6 +2146,10 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
     ta = w2 & 0xffffu;
     tb = w2 >> 16;
     tn = n2;
+    RMARK(5);  // the wait for the next tokens
+#ifdef SBAM_WAVE_STATS
+    rs_[6]++;  // steps
+#endif
 #else
     ta = ta2;
     tb = tb2;
@@ -2087,6 +2168,18 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
     if (Ft + lane < ae) ob[Ft + lane] = ring8[(Gr + (uint32_t)(Ft + lane)) & G::kMask];
   }
   if (__ballot(toofar) != 0 && lane == 0 && redo) redo[atomicAdd(nredo, 1u)] = (int32_t)b;
+#ifdef SBAM_WAVE_STATS
+  // slots 32..37: phases (the tail in 37 with the total's remainder), 38: steps, 39: rounds
+  const uint64_t tot_ = __builtin_amdgcn_s_memtime() - rt0_;
+  if (lane == 0) {
+    for (int i = 0; i < 6; i++) atomicAdd(&g_wave_stats[32 + i], (unsigned long long)rs_[i]);
+    atomicAdd(&g_wave_stats[38], (unsigned long long)rs_[6]);
+    atomicAdd(&g_wave_stats[39], (unsigned long long)rs_[7]);
+    atomicAdd(&g_wave_stats[31], (unsigned long long)tot_);
+    atomicAdd(&g_wave_stats[29], (unsigned long long)itw_);
+    atomicAdd(&g_wave_stats[30], (unsigned long long)itl_);
+  }
+#endif
 }
 
 __global__ void k_first_error(const int32_t *__restrict__ status, int64_t n, unsigned long long *first_err) {

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Diagnostic (tools-only build, `make -C spark-bam_amd EXTRA=-DSBAM_WAVE_STATS BUILD=build_stats`): cycle
-attribution inside k_inflate_wave (s_memtime per phase, summed over waves) on a synthetic BAM."""
+attribution inside k_inflate_wave and k_inflate_resolve (s_memtime per phase, summed over waves) on a synthetic BAM."""
 import ctypes
 import json
 import os
@@ -19,7 +19,7 @@ f = sbam.BamFile(s.bytes(), inflate=False)
 L = sbam.load_library()
 fn = L.sbam_debug_wave_stats
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
-buf = (ctypes.c_ulonglong * 32)()
+buf = (ctypes.c_ulonglong * 40)()
 f.reset(); f.run(contig_lengths=s.contig_lengths)
 fn(buf, 1)
 f.reset(); f.run(contig_lengths=s.contig_lengths)
@@ -42,4 +42,15 @@ out["b_iters_per_round"] = round(v[7] / max(v[6], 1), 3)
 out["rounds_per_block"] = round(v[6] / out["blocks"], 3)
 out["cycles_per_header"] = {n: round(v[i] / max(v[9], 1)) for i, n in ((0, "rest"), (10, "cl_setup"), (11, "chain"), (12, "stage"), (1, "build"))}
 out["cycles_per_round"] = {n: round(v[i] / max(v[6], 1)) for i, n in list(enumerate(names[2:6], 2)) + [(13, "warmup")]}
+rsteps = max(v[38], 1)
+rnames = ["positions_zero", "literals", "output_stores", "match_setup", "rounds", "token_wait"]
+res = {n: round(v[32 + i] / rsteps) for i, n in enumerate(rnames)}
+res["tail_and_rest"] = round((v[31] - sum(v[32:38])) / rsteps)
+out["resolve_cycles_per_step"] = res
+out["resolve_steps_per_block"] = round(v[38] / out["blocks"], 2)
+out["resolve_rounds_per_step"] = round(v[39] / rsteps, 3)
+out["resolve_cycles_per_block"] = round(v[31] / out["blocks"])
+out["resolve_ms"] = f.kernel_ms("inflate_resolve")
+out["resolve_copy_iters_per_step"] = {"wave": round(v[29] / rsteps, 2), "lane_sum": round(v[30] / rsteps, 2),
+                                      "lane_efficiency": round(v[30] / max(64 * v[29], 1), 3)}
 print(json.dumps(out))
