@@ -92,7 +92,38 @@ def test_ctypes_bindings_match_header_prototypes():
         assert got == want, (name, got, want)
 
 
+def test_reserve_rejects_bad_arguments_host_only():
+    """sbam_reserve checks its arguments before any device call: a null context or a negative size is
+    SBAM_ERR_ARG (no GPU needed)."""
+    import sbam
+    L = sbam.load_library()
+    assert L.sbam_reserve(None, 1 << 20, 16, 1 << 22, 0) == sbam.ERR_ARG
+    assert L.sbam_reserve(None, -1, 0, 0, 0) == sbam.ERR_ARG
+
+
 import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_reserve_then_larger_window_gpu():
+    """sbam_reserve sizes a context opened on a small file for a larger one; loading the larger file then gives
+    the same blocks, checker calls and full-check counts as a fresh context, and a negative size raises."""
+    import numpy as np
+    import sbam
+    from conftest import fixture_bytes
+    a, b = fixture_bytes("1.bam"), fixture_bytes("2.bam")
+    with sbam.BamFile(b) as fresh:
+        want_blocks = [x.copy() for x in fresh.blocks()]
+        want_calls = fresh.check_eager(0, fresh.uncompressed_size)
+        nb, ub = int(fresh.n_blocks), int(fresh.uncompressed_size)
+    with sbam.BamFile(a) as f:
+        f.reserve(2 * len(b), 2 * nb, 2 * ub, 0)
+        f.load(b)
+        f.run()
+        assert all(np.array_equal(x, y) for x, y in zip(f.blocks(), want_blocks))
+        assert np.array_equal(f.check_eager(0, f.uncompressed_size), want_calls)
+        with pytest.raises(sbam.SbamError):
+            f.reserve(-1, 0, 0, 0)
 
 
 @pytest.mark.gpu
