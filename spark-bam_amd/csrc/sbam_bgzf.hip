@@ -27,6 +27,9 @@ SB_DEV uint32_t brev(uint32_t code, int len) { return __builtin_bitreverse32(cod
 // 1. BGZF header scan
 // ================================================================================================
 constexpr int kScanThreads = 256;
+#ifndef SBAM_SCAN_PREFETCH  // k_scan_slots loads iteration i + 1 while ranking iteration i's candidates
+#define SBAM_SCAN_PREFETCH 1
+#endif
 constexpr int kScanStep = kScanThreads * 16;  // bytes per workgroup iteration
 
 // 16 candidate bits for positions q0..q0+15 given the 32 bytes at q0 (w[0..7] little-endian words).
@@ -177,15 +180,32 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_slots(const uint8_t *__re
   __shared__ int s_wsum[kScanThreads / 64];
   Candidate *out = slots + (int64_t)blockIdx.x * kScanSlots;
   int run = 0;
+#if SBAM_SCAN_PREFETCH
+  // the next iteration's 32 B are loaded before this one's candidates are ranked (two barriers), so a workgroup
+  // keeps 8 KiB in flight instead of 4
+  uint32_t wn[8];
+  if (cbase + threadIdx.x * 16 < cend) load32(d, cbase + threadIdx.x * 16, wn);
+#endif
   for (int64_t it = cbase; it < cend; it += kScanStep) {
     const int64_t q0 = it + threadIdx.x * 16;
     uint32_t bits = 0;
+#if SBAM_SCAN_PREFETCH
+    uint32_t w[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) w[k] = wn[k];
+    if (q0 + kScanStep < cend) load32(d, q0 + kScanStep, wn);
+    if (q0 < cend) {
+      bits = header_bits16(w, q0, D);
+      if (q0 + 16 > cend) bits &= (1u << (cend - q0)) - 1u;
+    }
+#else
     if (q0 < cend) {
       uint32_t w[8];
       load32(d, q0, w);
       bits = header_bits16(w, q0, D);
       if (q0 + 16 > cend) bits &= (1u << (cend - q0)) - 1u;
     }
+#endif
     if (threadIdx.x == 0) s_any = 0;
     __syncthreads();
     if (bits) s_any = 1;
