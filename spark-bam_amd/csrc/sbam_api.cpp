@@ -26,6 +26,8 @@ struct sbam_ctx {
   size_t comp_cap = 0;
   // list-form chain pass scratch (launch_chain_list_*)
   int32_t *d_ccnt = nullptr;
+  int32_t *d_tcnt = nullptr;  // record-0 pass: PASS0 positions per tile and wave (CountsDev::tile_pass0)
+  size_t tcnt_cap = 0;
   int64_t *d_coff2 = nullptr, *d_plist = nullptr, *d_pfb = nullptr;
   uint8_t *d_pok = nullptr;
   unsigned long long *d_nfb = nullptr;
@@ -273,6 +275,7 @@ void sbam_close(sbam_ctx *c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   dfree(c->d_comp);
   dfree(c->d_ccnt);
+  dfree(c->d_tcnt);
   dfree(c->d_coff2);
   dfree(c->d_plist);
   dfree(c->d_pfb);
@@ -390,6 +393,7 @@ int sbam_reserve(sbam_ctx *c, int64_t comp_bytes, int64_t n_blocks, int64_t ubyt
   HIPCHK(c, ensure(&c->d_tokbase, &c->tokbase_cap, n_blocks));
   HIPCHK(c, ensure(&c->d_slow, &c->slow_cap, n_blocks));
   if (int rc = ensure_bitmap(c, 0, ubytes)) return rc;
+  HIPCHK(c, ensure(&c->d_tcnt, &c->tcnt_cap, (size_t)(4 * check_tiles(0, ubytes) + 8)));  // (x0 may add a tile)
   if (n_records > 0) {  // the chain pass's PASS0 list (about one entry per record) and loadReads' offsets
     const size_t n = (size_t)(n_records + n_records / 8 + 4096);
     HIPCHK(c, ensure(&c->d_plist, &c->plist_cap, n));
@@ -780,7 +784,8 @@ static int check_range_args(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R) {
   return SBAM_OK;
 }
 
-static hipError_t run_chains(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd);
+static hipError_t run_chains(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,
+                             const int32_t *tile_pass0 = nullptr);
 
 int sbam_check_eager(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, uint64_t *bitmap) {
   if (!c) return SBAM_ERR_ARG;
@@ -835,14 +840,15 @@ int sbam_check_full_words(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, uint32
 
 // Chain pass after a record-0 pass: the list form (launch_chain_list_*) when the PASS0 positions fit its
 // scratch (a position list of up to 1/32 of the range), else the per-chunk k_chains walk.
-static hipError_t run_chains(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd) {
+static hipError_t run_chains(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,
+                             const int32_t *tile_pass0) {
   const int64_t nch = chain_list_chunks(x0, x1);
   const int64_t cap = (x1 - x0) / 32 + 4096;
   hipError_t e;
   if ((e = ensure(&c->d_ccnt, &c->ccnt_cap, (size_t)std::max<int64_t>(nch, 1))) != hipSuccess) return e;
   if ((e = ensure(&c->d_coff2, &c->coff2_cap, (size_t)nch + 1)) != hipSuccess) return e;
   ChainScratch cs{c->d_ccnt, c->d_coff2, nullptr, nullptr, nullptr, nullptr};
-  if ((e = launch_chain_list_build(x0, x1, c->d_bitmap, cs, c->stream)) != hipSuccess) return e;
+  if ((e = launch_chain_list_build(x0, x1, c->d_bitmap, cs, tile_pass0, c->stream)) != hipSuccess) return e;
   int64_t total = 0;
   if ((e = hipMemcpyAsync(&total, c->d_coff2 + nch, 8, hipMemcpyDeviceToHost, c->stream)) != hipSuccess) return e;
   if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return e;
@@ -877,14 +883,17 @@ int sbam_check_full_counts(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, int32
   cd.pair = cd.rbe + 21 * 128;
   cd.scalars = cd.pair + 19 * 19;
   cd.totals = cd.scalars + 4;
+  HIPCHK(c, ensure(&c->d_tcnt, &c->tcnt_cap, (size_t)std::max<int64_t>(4 * check_tiles(x0, x1), 1)));
+  cd.tile_pass0 = c->d_tcnt;
+  bool tiles = false;
   {
     Timer t(c, "check_full");
     {
       Timer t0(c, "check_pass0");
-      HIPCHK(c, launch_check_full_counts(view(c), x0, x1, R, by_key, cd, c->d_bitmap, c->stream));
+      HIPCHK(c, launch_check_full_counts(view(c), x0, x1, R, by_key, cd, c->d_bitmap, c->stream, &tiles));
     }
     Timer t1(c, "check_chains");
-    HIPCHK(c, run_chains(c, x0, x1, R, by_key, cd));
+    HIPCHK(c, run_chains(c, x0, x1, R, by_key, cd, tiles ? c->d_tcnt : nullptr));
   }
   std::vector<unsigned long long> h(kCountsWords);
   HIPCHK(c, hipMemcpyAsync(h.data(), c->d_counts, kCountsWords * 8, hipMemcpyDeviceToHost, c->stream));

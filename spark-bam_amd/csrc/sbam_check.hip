@@ -363,6 +363,18 @@ __global__ __launch_bounds__(256) void k_p0_count(const unsigned long long *__re
   if (threadIdx.x == 0) chunk_cnt[blockIdx.x] = (int32_t)(s_c[0] + s_c[1] + s_c[2] + s_c[3]);
 }
 
+// The same counts from the record-0 pass's per-tile, per-wave counts (k_check_bits / k_check<MODE_COUNTS, 2>): a chunk
+// is 16 whole tiles, so its count is 64 integers instead of 16 KiB of bitmap.
+__global__ __launch_bounds__(256) void k_p0_count_tiles(const int32_t *__restrict__ tile_pass0, int64_t ntiles,
+                                                        int64_t nch, int32_t *__restrict__ chunk_cnt) {
+  const int64_t ch = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= nch) return;
+  const int64_t t0 = ch * 16, t1 = min(t0 + 16, ntiles);
+  int32_t c = 0;
+  for (int64_t i = 4 * t0; i < 4 * t1; i++) c += tile_pass0[i];
+  chunk_cnt[ch] = c;
+}
+
 // exclusive scan of the chunk counts (one workgroup): off[ch], and off[n] = total
 __global__ __launch_bounds__(1024) void k_p0_scan(const int32_t *__restrict__ cnt, int64_t n, int64_t *__restrict__ off) {
   __shared__ int64_t s_w[16];
@@ -918,6 +930,8 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
     const Tile tl{s_win, s_opc, s_nbad, base};
     const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
     uint32_t hkp[3] = {0, 0, 0}, hpl[3] = {0, 0, 0};  // held compressed counts of an even group (add4_paired)
+    constexpr bool TILECNT = MODE == MODE_COUNTS && PART == 2;  // boundary tiles of the bit-sliced pass
+    uint32_t tc = 0;                                             // PASS0 positions of the words this lane writes
     auto run_tile = [&](auto interior_tag) {
     constexpr bool INTERIOR = decltype(interior_tag)::value;
 #pragma unroll 1
@@ -960,6 +974,7 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
       } else if ((lane & 15) == 0 && xg < x1) {
         bitmap[(xg - x0a) >> 6] = v;  // word holds >= 1 position < x1
       }
+      if (TILECNT && (lane & 15) == 0 && (INTERIOR || xg < x1)) tc += (uint32_t)__popcll(v);
       if (!COUNTS) continue;
       uint32_t Fo[4];
       if constexpr (INTERIOR && !BYKEY) {
@@ -1000,6 +1015,10 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
       if (base >= x0 && base + kTile <= x1 && base + kTile + kInteriorTail <= sv.L)
         run_tile(std::integral_constant<bool, true>{});
       else run_tile(std::integral_constant<bool, false>{});
+    }
+    if (TILECNT && cd.tile_pass0) {
+      const uint32_t c = wave_sum(tc);
+      if (lane == 0) cd.tile_pass0[t * 4 + (int)(threadIdx.x >> 6)] = (int32_t)c;
     }
     if (COUNTS) {
       if (++since_flush == kFlushTiles) {
@@ -1303,6 +1322,10 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bi
     P = nibble_xpose_stage<2>(P, li);
     P = nibble_xpose_stage<1>(P, li);
     reinterpret_cast<uint32_t *>(bitmap)[((base - x0a) >> 5) + 32 * li + (t >> 3)] = P;
+    if (cd.tile_pass0) {  // the chain pass's counts: this wave's PASS0 positions of the tile
+      const uint32_t c = wave_sum((uint32_t)__popc(P));
+      if (lane == 0) cd.tile_pass0[(tlo + ti) * 4 + (t >> 6)] = (int32_t)c;
+    }
   }
   // per-lane counters -> workgroup -> device
   flush_cnt();
@@ -1610,14 +1633,18 @@ static int chain_grid(int64_t x0, int64_t x1) {
   return (int)(g < 1 ? 1 : g > 65535 ? 65535 : g);
 }
 
+int64_t check_tiles(int64_t x0, int64_t x1) { return x1 > x0 ? ntiles_of(x0, x1) : 0; }
 hipError_t launch_check_full_counts(StreamView sv, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,
-                                    unsigned long long *bitmap, hipStream_t s) {
+                                    unsigned long long *bitmap, hipStream_t s, bool *tiles_counted) {
+  *tiles_counted = false;
   if (x1 <= x0) return hipSuccess;
   if (by_key) {
     hipLaunchKernelGGL((k_check<MODE_BYKEY, 0>), dim3(check_grid(ntiles_of(x0, x1))), dim3(kCheckThreads), 0, s, sv,
                        x0, x1, R, cd, bitmap, nullptr, (int64_t)0, (int64_t)0);
   } else if (R > 0 && sv.nref <= kLdsLens) {
-    // interior tiles bit-sliced (k_check_bits), the boundary tiles by k_check<MODE_COUNTS, 2>
+    // interior tiles bit-sliced (k_check_bits), the boundary tiles by k_check<MODE_COUNTS, 2>; between them every
+    // tile's PASS0 count when cd.tile_pass0 is set
+    *tiles_counted = cd.tile_pass0 != nullptr;
     int64_t tlo, thi;
     interior_tiles(sv, x0, x1, &tlo, &thi);
     const int64_t nt = ntiles_of(x0, x1), ni = thi - tlo;
@@ -1645,11 +1672,16 @@ int64_t chain_list_chunks(int64_t x0, int64_t x1) {
   const int64_t words = (x1 - (x0 & ~(int64_t)63) + 63) >> 6;
   return (words + kChainWords - 1) / kChainWords;
 }
+static_assert(kChainWords * 64 == 16 * kTile, "a chain chunk is 16 record-0 tiles");
 hipError_t launch_chain_list_build(int64_t x0, int64_t x1, const unsigned long long *bitmap, const ChainScratch &cs,
-                                   hipStream_t s) {
+                                   const int32_t *tile_pass0, hipStream_t s) {
   const int64_t x0a = x0 & ~(int64_t)63, nwords = (x1 - x0a + 63) >> 6, nch = chain_list_chunks(x0, x1);
   if (nch <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_p0_count, dim3((unsigned)nch), dim3(256), 0, s, bitmap, nwords, cs.chunk_cnt);
+  if (tile_pass0)
+    hipLaunchKernelGGL(k_p0_count_tiles, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, s, tile_pass0,
+                       ntiles_of(x0, x1), nch, cs.chunk_cnt);
+  else
+    hipLaunchKernelGGL(k_p0_count, dim3((unsigned)nch), dim3(256), 0, s, bitmap, nwords, cs.chunk_cnt);
   hipLaunchKernelGGL(k_p0_scan, dim3(1), dim3(1024), 0, s, cs.chunk_cnt, nch, cs.chunk_off);
   return hipGetLastError();
 }

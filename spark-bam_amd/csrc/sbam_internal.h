@@ -56,6 +56,9 @@ struct CountsDev {  // mirrors sbam_counts (int64 fields) in device memory
   unsigned long long *pair;  // [19][19]
   unsigned long long *scalars;  // n_positions, n_success, n_too_few_fixed, n_halo
   unsigned long long *totals;   // [19] per-flag totals over every counted position
+  // [ntiles][4]: the record-0 pass's PASS0 positions per tile and wave (set only for the bit-sliced pass, which then
+  // writes every tile's; the chain pass's chunk counts come from these instead of a second read of the bitmap)
+  int32_t *tile_pass0 = nullptr;
 };
 
 // Device columns of decoded records (sbam_records.hip); mirrors sbam_record_columns minus the offsets.
@@ -114,8 +117,10 @@ hipError_t launch_inflate_redo(const uint8_t *d, int64_t D, BlockTable bt, TokPo
 hipError_t launch_first_error(const int32_t *status, int64_t n, unsigned long long *first_err, hipStream_t s);
 hipError_t launch_lower_bound(const Candidate *c, int64_t n, int64_t q, int64_t *out, hipStream_t s);
 // Bitmaps cover [x0 & ~63, x1): bit (x - (x0 & ~63)) = call at x (0 for x < x0).
+// *tiles_counted: whether cd.tile_pass0 now holds every tile's PASS0 count (the bit-sliced pass ran)
 hipError_t launch_check_full_counts(StreamView sv, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,
-                                    unsigned long long *bitmap, hipStream_t s);
+                                    unsigned long long *bitmap, hipStream_t s, bool *tiles_counted);
+int64_t check_tiles(int64_t x0, int64_t x1);  // record-0 pass tiles of [x0, x1)
 // (launch_check_full_counts runs the record-0 pass; launch_check_full_chains then resolves the PASS0 chains)
 hipError_t launch_check_full_chains(StreamView sv, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,
                                     unsigned long long *bitmap, hipStream_t s);
@@ -129,8 +134,9 @@ struct ChainScratch {
   unsigned long long *n_fb;       // fallback count
 };
 int64_t chain_list_chunks(int64_t x0, int64_t x1);
+// tile_pass0 (or nullptr: count the bitmap): the record-0 pass's per-tile counts (CountsDev::tile_pass0)
 hipError_t launch_chain_list_build(int64_t x0, int64_t x1, const unsigned long long *bitmap, const ChainScratch &cs,
-                                   hipStream_t s);
+                                   const int32_t *tile_pass0, hipStream_t s);
 hipError_t launch_chain_list_run(StreamView sv, int64_t x0, int64_t x1, int32_t R, int32_t by_key, CountsDev cd,
                                  unsigned long long *bitmap, const ChainScratch &cs, hipStream_t s);
 hipError_t launch_check_eager_pass0(StreamView sv, int64_t x0, int64_t x1, int32_t R, unsigned long long *bitmap,
