@@ -472,6 +472,46 @@ __global__ __launch_bounds__(256) void k_p0_fast(const int64_t *__restrict__ lis
   }
 }
 
+// The same for 2 <= R <= 10, 16 entries per thread: the 24 link bytes ok[i0, i0 + 24) become a 24-bit mask (one
+// 16-B and one 8-B load instead of R - 1 byte loads per entry), and entry j succeeds when its R - 1 bits from j hold.
+__global__ __launch_bounds__(256) void k_p0_fast16(const int64_t *__restrict__ list, const int64_t *__restrict__ n_ptr,
+                                                   const uint8_t *__restrict__ ok, int R, CountsDev cd,
+                                                   int64_t *__restrict__ fb, unsigned long long *__restrict__ n_fb) {
+  const int64_t n = *n_ptr;
+  const uint32_t need = (1u << (R - 1)) - 1u;  // R - 1 consecutive links
+  uint32_t n_succ = 0, n_gap = 0;
+  auto nib = [](uint32_t w) { return (((w & 0x01010101u) * 0x00204081u) >> 21) & 0xfu; };  // byte k != 0 -> bit k
+  for (int64_t i0 = 16 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); i0 < n;
+       i0 += 16 * (int64_t)gridDim.x * blockDim.x) {
+    uint32_t m = 0;
+    if (i0 + 24 <= n) {
+      const uint4 a = *reinterpret_cast<const uint4 *>(ok + i0);
+      const uint2 b = *reinterpret_cast<const uint2 *>(ok + i0 + 16);
+      m = nib(a.x) | nib(a.y) << 4 | nib(a.z) << 8 | nib(a.w) << 12 | nib(b.x) << 16 | nib(b.y) << 20;
+    } else {
+      for (int k = 0; k < 24 && i0 + k < n; k++) m |= (ok[i0 + k] != 0 ? 1u : 0u) << k;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const int64_t i = i0 + j;
+      if (i < n) {
+        const bool succ = i + (R - 1) <= n - 1 && ((m >> j) & need) == need;
+        if (succ) n_succ++;
+        else fb[atomicAdd(n_fb, 1ull)] = list[i];
+        n_gap += (i + 1 < n && !((m >> j) & 1u)) ? 1u : 0u;
+      }
+    }
+  }
+  if (__ballot(n_gap != 0)) {
+    n_gap = wave_sum(n_gap);
+    if (lane_id() == 0) atomicAdd(&n_fb[1], (unsigned long long)n_gap);
+  }
+  if (cd.counts) {
+    n_succ = wave_sum(n_succ);
+    if (lane_id() == 0 && n_succ) atomicAdd(&cd.scalars[1], (unsigned long long)n_succ);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_p0_fallback(StreamView sv, int64_t x0a, int64_t x1, int R,
                                                      unsigned long long *__restrict__ bitmap, CountsDev cd, int bykey,
                                                      const int64_t *__restrict__ fb,
@@ -1693,7 +1733,10 @@ hipError_t launch_chain_list_run(StreamView sv, int64_t x0, int64_t x1, int32_t 
   hipLaunchKernelGGL(k_p0_list, dim3((unsigned)nch), dim3(256), 0, s, bitmap, nwords, x0a, cs.chunk_off, cs.list);
   hipLaunchKernelGGL(k_p0_links, dim3(4096), dim3(256), 0, s, sv, cs.list, n_ptr, cs.ok);
   (void)hipMemsetAsync(cs.n_fb, 0, 3 * sizeof(unsigned long long), s);  // fallbacks, missing links, failed fallbacks
-  hipLaunchKernelGGL(k_p0_fast, dim3(4096), dim3(256), 0, s, cs.list, n_ptr, cs.ok, (int)R, cd, cs.fb, cs.n_fb);
+  if (R >= 2 && R <= 10)
+    hipLaunchKernelGGL(k_p0_fast16, dim3(1024), dim3(256), 0, s, cs.list, n_ptr, cs.ok, (int)R, cd, cs.fb, cs.n_fb);
+  else
+    hipLaunchKernelGGL(k_p0_fast, dim3(4096), dim3(256), 0, s, cs.list, n_ptr, cs.ok, (int)R, cd, cs.fb, cs.n_fb);
   hipLaunchKernelGGL(k_p0_fallback, dim3(1024), dim3(256), 0, s, sv, x0a, x1, (int)R, bitmap, cd, (int)by_key, cs.fb,
                      cs.n_fb);
   return hipGetLastError();
