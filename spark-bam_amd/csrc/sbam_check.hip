@@ -375,32 +375,34 @@ __global__ __launch_bounds__(256) void k_p0_count_tiles(const int32_t *__restric
   chunk_cnt[ch] = c;
 }
 
-// exclusive scan of the chunk counts (one workgroup): off[ch], and off[n] = total
+// exclusive scan of the chunk counts (one workgroup): off[ch], and off[n] = total.  Thread t owns the contiguous run
+// [t·per, (t + 1)·per) of the counts: it sums its run, one workgroup scan of the 1024 sums gives every run its
+// base, and the run is written out (two passes over n integers instead of n / 1024 barrier-separated rounds:
+// 311 -> ~20 us for the 206 K chunks of a 10 GB shard).
 __global__ __launch_bounds__(1024) void k_p0_scan(const int32_t *__restrict__ cnt, int64_t n, int64_t *__restrict__ off) {
   __shared__ int64_t s_w[16];
-  __shared__ int64_t s_carry;
-  if (threadIdx.x == 0) s_carry = 0;
-  __syncthreads();
   const int lane = lane_id(), wv = threadIdx.x >> 6;
-  for (int64_t b = 0; b < n; b += 1024) {
-    const int64_t i = b + threadIdx.x;
-    const int64_t v = i < n ? cnt[i] : 0;
-    int64_t incl = v;
+  const int64_t per = (n + 1023) / 1024;
+  const int64_t b = min((int64_t)threadIdx.x * per, n), e = min(b + per, n);
+  int64_t sum = 0;
+#pragma unroll 8
+  for (int64_t i = b; i < e; i++) sum += cnt[i];
+  int64_t incl = sum;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int64_t t = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += t;
-    }
-    if (lane == 63) s_w[wv] = incl;
-    __syncthreads();
-    int64_t before = s_carry;
-    for (int k = 0; k < wv; k++) before += s_w[k];
-    if (i < n) off[i] = before + incl - v;
-    __syncthreads();
-    if (threadIdx.x == 1023) s_carry = before + incl;
-    __syncthreads();
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
   }
-  if (threadIdx.x == 0) off[n] = s_carry;
+  if (lane == 63) s_w[wv] = incl;
+  __syncthreads();
+  int64_t run = incl - sum;
+  for (int k = 0; k < wv; k++) run += s_w[k];
+#pragma unroll 8
+  for (int64_t i = b; i < e; i++) {
+    off[i] = run;
+    run += cnt[i];
+  }
+  if (threadIdx.x == 1023) off[n] = run;  // (thread 1023's run ends at n: b and e are clamped to n)
 }
 
 __global__ __launch_bounds__(256) void k_p0_list(const unsigned long long *__restrict__ bitmap, int64_t nwords,
