@@ -126,7 +126,23 @@ __global__ void k_split_popcounts(const unsigned long long *__restrict__ bm, int
   if (a >= 0 && a < b) {
     const int64_t ra = a - xa, rb = b - xa;
     const int64_t wa = ra >> 6, wb = (rb - 1) >> 6;
-    for (int64_t w = wa + threadIdx.x; w <= wb; w += blockDim.x) {
+    // 8 words in flight per thread (as a one-word loop each load waited for the one before: 0.68 ms per 10 GB)
+    const int64_t step = blockDim.x;
+    int64_t w = wa + threadIdx.x;
+    for (; w + 7 * step <= wb; w += 8 * step) {
+      unsigned long long m[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) m[k] = bm[w + k * step];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int64_t wk = w + k * step;
+        unsigned long long x = m[k];
+        if (wk == wa) x &= ~0ull << (ra & 63);
+        if (wk == wb) x &= ~0ull >> (63 - ((rb - 1) & 63));
+        c += __popcll(x);
+      }
+    }
+    for (; w <= wb; w += step) {
       unsigned long long m = bm[w];
       if (w == wa) m &= ~0ull << (ra & 63);
       if (w == wb) m &= ~0ull >> (63 - ((rb - 1) & 63));
