@@ -117,11 +117,21 @@ def shard_pass(f, p: ShardPlan, split_size: int, R: int = 10) -> ShardResult:
                        n.astype(np.int64))
 
 
-def shard_load(f, p: ShardPlan, split_size: int, R: int = 10, use_success_bitmap: bool = False) -> np.ndarray:
+def shard_load(f, p: ShardPlan, split_size: int, R: int = 10, use_success_bitmap: bool = False,
+               eager_proof: bool = True) -> np.ndarray:
     """One shard's loadReads: the owned Hadoop splits' records decoded into device columns
-    (sbam_load_records; CanLoadBam.scala:281-334); returns the partition sizes."""
+    (sbam_load_records; CanLoadBam.scala:281-334); returns the partition sizes.
+
+    eager_proof: first run the eager checker over the shard (its calls' bitmap stays on the device) so that the
+    splits' record chains come from that bitmap once sbam_load_records has proved it — every set bit from a
+    split's first record hops (block_size) to the next set bit — instead of one lane walking each split's chain
+    record by record (twice: counts, then offsets).  The records are the same either way: a bitmap that fails
+    the proof falls back to the walk."""
     if not p.split_count:
         return np.zeros(0, np.int64)
+    if eager_proof and not use_success_bitmap:
+        f.check_eager_device(0, f.uncompressed_size, R)
+        use_success_bitmap = True
     sizes, _ = f.load_records(split_size, first=p.split_first, count=p.split_count, reads_to_check=R,
                               use_success_bitmap=use_success_bitmap, columns=None)
     return sizes
@@ -201,8 +211,9 @@ class GpuShard:
             p = self.plan
             if not p.split_count:
                 return np.zeros(0, np.int64), {k: np.zeros(0, self.sbam.RECORD_COLUMNS[k]) for k in columns}
+            self.f.check_eager_device(0, self.f.uncompressed_size, self.R)  # (shard_load's eager_proof)
             return self.f.load_records(self.split_size, first=p.split_first, count=p.split_count,
-                                       reads_to_check=self.R, columns=columns)
+                                       reads_to_check=self.R, use_success_bitmap=True, columns=columns)
         return self._retry(once)
 
     def close(self):

@@ -38,8 +38,10 @@ def check_columns(o, offs, cols):
 
 @pytest.mark.parametrize("name", INDEXED_BAMS)
 @pytest.mark.parametrize("split_kb", [20, 100, 2048])
-@pytest.mark.parametrize("bitmap", [False, True])
+@pytest.mark.parametrize("bitmap", [False, True, "eager"])
 def test_load_records_vs_oracle(name, split_kb, bitmap, gpu_files, oracle_files):
+    """bitmap: False = the chain walk; True = the full check's success bitmap; "eager" = the eager checker's calls
+    (what the sharded loadReads uses, sbam.dist.shard_load)."""
     g, o = gpu_files(name), oracle_files(name)
     S = split_kb * 1024
     try:
@@ -48,9 +50,11 @@ def test_load_records_vs_oracle(name, split_kb, bitmap, gpu_files, oracle_files)
         with pytest.raises(Exception):
             g.load_records(S)
         return
-    if bitmap:
+    if bitmap == "eager":
+        g.check_eager_device(0, g.uncompressed_size)
+    elif bitmap:
         g.check_full_counts(0, g.uncompressed_size)
-    got_sizes, cols = g.load_records(S, use_success_bitmap=bitmap)
+    got_sizes, cols = g.load_records(S, use_success_bitmap=bool(bitmap))
     assert got_sizes.tolist() == sizes
     check_columns(o, offs, cols)
 
@@ -126,5 +130,8 @@ def test_synthetic_1gb_properties():
         sp, cp = g.load_records(S, use_success_bitmap=True, columns=("offset", "block_size"))
         assert np.array_equal(sw, sp) and np.array_equal(cw["offset"], cp["offset"])
         assert int(sp.sum()) == s.n_records
+        g.check_eager_device(0, g.uncompressed_size)  # the eager calls' bitmap proves the same chains
+        se, ce = g.load_records(S, use_success_bitmap=True, columns=("offset", "block_size"))
+        assert np.array_equal(sw, se) and np.array_equal(cw["offset"], ce["offset"])
         off, bs = cp["offset"], cp["block_size"].astype(np.int64)
         assert np.array_equal(off[1:], off[:-1] + 4 + bs[:-1])
