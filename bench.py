@@ -239,6 +239,8 @@ def main():
         f"workload {args.workload}, setup {time.time() - t:.1f}s, host threads {threads} of {nproc}")
     kernels = ("scan", "chain", "inflate", "inflate_decode", "inflate_resolve", "check_full", "check_pass0",
                "check_chains", "find_record", "records", "load_records")
+    if args.workload == "load-reads":  # (the eager calls whose bitmap proves the splits' record chains)
+        kernels += ("check_eager",)
     last = {}
 
     def run_window(sh):
