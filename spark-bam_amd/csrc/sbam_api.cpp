@@ -1005,13 +1005,31 @@ static int split_starts(sbam_ctx *c, const sbam_split_args *a, int64_t first, in
   if (rc) return rc;
   std::vector<int64_t> x0(count);
   xe.assign(count, 0);
+  // block_at / x_end_of for every split: the queries ascend, so each search gallops from the previous answer
+  // (10 240 independent binary searches over the host block table took ~1 ms of host time per 10 GB step)
+  const int64_t nbh = (int64_t)c->h_bstart.size();
+  auto first_ge = [&](int64_t from, int64_t q) {  // first index >= from with h_bstart[index] >= q
+    int64_t lo = from, step = 1, hi = from;
+    while (hi < nbh && c->h_bstart[hi] < q) {
+      lo = hi + 1;
+      hi += step;
+      step *= 2;
+    }
+    return (int64_t)(std::lower_bound(c->h_bstart.begin() + lo, c->h_bstart.begin() + std::min(hi, nbh), q) -
+                     c->h_bstart.begin());
+  };
+  int64_t ib = 0, ie = 0;
   for (int64_t i = 0; i < count; i++) {
-    const int64_t b = block_at(c, bs[i] - c->base);
+    const int64_t qb = bs[i] - c->base, qe = en[first + i] - c->base;
+    const bool sorted = i == 0 || (bs[i] >= bs[i - 1] && en[first + i] >= en[first + i - 1]);
+    ib = first_ge(sorted ? ib : 0, qb);
+    ie = first_ge(sorted ? ie : 0, qe);
+    const int64_t b = (ib < nbh && c->h_bstart[ib] == qb) ? ib : -1;  // block_at
     if (b < 0) {  // FindRecordStart on the EOF marker: empty stream → None → NoReadFoundException
       return no_read_found(c, bs[i], a->max_read_size);
     }
     x0[i] = c->h_buoff[b];
-    xe[i] = x_end_of(c, en[first + i] - c->base);
+    xe[i] = ie < nbh ? c->h_buoff[ie] : c->L;  // x_end_of
   }
   rc = find_record_starts(c, x0, a->reads_to_check, a->max_read_size, a->use_success_bitmap != 0, xs);
   if (rc) return rc;
