@@ -255,6 +255,13 @@ class Counts:
         return {FLAG_NAMES[i]: int(t[i]) for i in range(19)}
 
 
+def n_hadoop_splits(file_size: int, split_size: int) -> int:
+    """len(hadoop_splits(...)) without building the list (a 10 GB file has ~5000 splits)."""
+    n = ctypes.c_int64(0)
+    load_library().sbam_file_splits(file_size, split_size, None, None, 0, ctypes.byref(n))
+    return int(n.value)
+
+
 def hadoop_splits(file_size: int, split_size: int):
     """FileInputFormat split rule (through libsbam.sbam_file_splits)."""
     L = load_library()
@@ -514,7 +521,7 @@ class BamFile:
                              max_read_size: int = MAX_READ_SIZE, use_success_bitmap: bool = False):
         """split_records as arrays (first record block_pos, offset, non-empty, record count): no per-split
         Python objects (a 10 GB file has ~5000 splits)."""
-        ns = len(hadoop_splits(self.file_size, split_size))
+        ns = n_hadoop_splits(self.file_size, split_size)
         count = ns - first if count is None else count
         fp = np.zeros(max(count, 1), dtype=[("block_pos", "<i8"), ("offset", "<i4"), ("reserved", "<i4")])
         fd = np.zeros(max(count, 1), np.int32)
@@ -534,7 +541,7 @@ class BamFile:
                        use_success_bitmap: bool = False) -> List[Split]:
         """loadSplitsAndReads(...).splits (CanLoadBam.scala:245-279)."""
         a = self._args(split_size, bgzf_blocks_to_check, reads_to_check, max_read_size, use_success_bitmap)
-        cap = len(hadoop_splits(self.file_size, split_size)) + 1
+        cap = n_hadoop_splits(self.file_size, split_size) + 1
         out = (_Split * cap)()
         n = ctypes.c_int64(0)
         self._check(self.L.sbam_compute_splits(self.ctx, ctypes.byref(a), ctypes.addressof(out), cap,
@@ -555,7 +562,7 @@ class BamFile:
         """Records of Hadoop splits [first, first+count) decoded on the GPU (sbam_load_records): returns
         (partition sizes, {column: ndarray}) with the records of all those splits concatenated in split order.
         `columns=None` leaves the columns on the device (count only)."""
-        ns = len(hadoop_splits(self.file_size, split_size))
+        ns = n_hadoop_splits(self.file_size, split_size)
         count = ns - first if count is None else count
         sizes = np.zeros(max(count, 1), np.int64)
         n = ctypes.c_int64(0)
