@@ -215,12 +215,6 @@ int64_t block_at(const sbam_ctx *c, int64_t q) {
   if (it == c->h_bstart.end() || *it != q) return -1;
   return it - c->h_bstart.begin();
 }
-// flat offset of Pos(end, 0) for relative compressed offset q: first block with start >= q
-int64_t x_end_of(const sbam_ctx *c, int64_t q) {
-  auto it = std::lower_bound(c->h_bstart.begin(), c->h_bstart.end(), q);
-  if (it == c->h_bstart.end()) return c->L;
-  return c->h_buoff[it - c->h_bstart.begin()];
-}
 sbam_pos pos_of(const sbam_ctx *c, int64_t x) {
   // last block with uoff <= x and usize > 0 containing x; x at a block end normalises to (next, 0)
   auto it = std::upper_bound(c->h_buoff.begin(), c->h_buoff.begin() + c->nblocks, x);
@@ -1029,7 +1023,7 @@ static int split_starts(sbam_ctx *c, const sbam_split_args *a, int64_t first, in
       return no_read_found(c, bs[i], a->max_read_size);
     }
     x0[i] = c->h_buoff[b];
-    xe[i] = ie < nbh ? c->h_buoff[ie] : c->L;  // x_end_of
+    xe[i] = ie < nbh ? c->h_buoff[ie] : c->L;  // flat offset of Pos(first block starting at or past the end, 0)
   }
   rc = find_record_starts(c, x0, a->reads_to_check, a->max_read_size, a->use_success_bitmap != 0, xs);
   if (rc) return rc;

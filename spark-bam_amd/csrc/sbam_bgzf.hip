@@ -30,6 +30,9 @@ constexpr int kScanThreads = 256;
 #ifndef SBAM_SCAN_PREFETCH  // k_scan_slots loads iteration i + 1 while ranking iteration i's candidates
 #define SBAM_SCAN_PREFETCH 1
 #endif
+#ifndef SBAM_SCAN_WIDE  // k_scan_slots_wide<SBAM_SCAN_WIDE> (positions per thread and iteration) instead of
+#define SBAM_SCAN_WIDE 32  // k_scan_slots (0); scan at 10 GB: 16 / 32 / 64 -> 2.51 / 2.14 / 2.20 ms, k_scan_slots 2.83
+#endif
 constexpr int kScanStep = kScanThreads * 16;  // bytes per workgroup iteration
 
 // 16 candidate bits for positions q0..q0+15 given the 32 bytes at q0 (w[0..7] little-endian words).
@@ -238,6 +241,86 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_slots(const uint8_t *__re
   }
 }
 
+// Wide form of k_scan_slots: P positions per thread and iteration (P + 16 B loaded as 16-B pieces, the next one's
+// prefetched while this one's candidates are ranked), and one barrier per iteration without candidates (an
+// "any candidate" flag in three rotating LDS words: the one for iteration i + 1 is cleared before iteration i's
+// barrier, after every read of it in iteration i - 2).  Same slots, counts and overflow as k_scan_slots.
+template <int P>
+SB_DEV void load_wide(const uint8_t *d, int64_t q0, uint32_t w[P / 4 + 4]) {
+#pragma unroll
+  for (int k = 0; k < P / 16 + 1; k++) {
+    const uint4 a = *reinterpret_cast<const uint4 *>(d + q0 + 16 * k);
+    w[4 * k] = a.x; w[4 * k + 1] = a.y; w[4 * k + 2] = a.z; w[4 * k + 3] = a.w;
+  }
+}
+template <int P>
+__global__ __launch_bounds__(kScanThreads) void k_scan_slots_wide(const uint8_t *__restrict__ d, int64_t D,
+                                                                   int32_t *__restrict__ chunk_counts,
+                                                                   Candidate *__restrict__ slots,
+                                                                   unsigned long long *__restrict__ overflow) {
+  constexpr int kW = P / 4 + 4, kScanWideStep = kScanThreads * P;  // words per thread, bytes per iteration
+  static_assert(P % 16 == 0 && P <= 64 && kScanChunk % kScanWideStep == 0 && kCompPad >= P + 16, "wide scan");
+  const int64_t cbase = (int64_t)blockIdx.x * kScanChunk;
+  const int64_t cend = min(cbase + (int64_t)kScanChunk, D);
+  __shared__ int s_any[3];
+  __shared__ int s_wsum[kScanThreads / 64];
+  if (threadIdx.x < 3) s_any[threadIdx.x] = 0;
+  __syncthreads();
+  Candidate *out = slots + (int64_t)blockIdx.x * kScanSlots;
+  int run = 0, ph = 0;
+  uint32_t wn[kW];
+  if (cbase + threadIdx.x * P < cend) load_wide<P>(d, cbase + threadIdx.x * P, wn);
+  for (int64_t it = cbase; it < cend; it += kScanWideStep) {
+    const int64_t q0 = it + threadIdx.x * P;
+    uint32_t w[kW];
+#pragma unroll
+    for (int k = 0; k < kW; k++) w[k] = wn[k];
+    if (q0 + kScanWideStep < cend) load_wide<P>(d, q0 + kScanWideStep, wn);
+    uint64_t bits = 0;
+    if (q0 < cend) {
+#pragma unroll
+      for (int i = 0; i < P; i++) {
+        const int wi = i >> 2, o = i & 3;
+        const uint32_t m = __builtin_amdgcn_alignbyte(w[wi + 1], w[wi], o);
+        const uint32_t bc = __builtin_amdgcn_alignbyte(w[wi + 4], w[wi + 3], o) & 0x00ffffffu;
+        bits |= (m == 0x04088b1fu && bc == 0x00024342u) ? (1ull << i) : 0ull;
+      }
+      // Header.make needs 18 bytes; the chunk owns positions below cend
+      const int64_t lim = min(cend - q0, D - 18 + 1 - q0);
+      if (lim < P) bits &= lim > 0 ? (1ull << lim) - 1ull : 0ull;
+    }
+    const int nx = ph == 2 ? 0 : ph + 1;
+    if (threadIdx.x == 0) s_any[nx] = 0;
+    if (bits) s_any[ph] = 1;
+    __syncthreads();
+    const bool any = s_any[ph] != 0;
+    ph = nx;
+    if (any) {  // rare: ordered rank = wave prefix + preceding waves
+      const int c = __popcll(bits);
+      int incl = c;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (lane_id() >= o) incl += t;
+      }
+      if (lane_id() == 63) s_wsum[threadIdx.x >> 6] = incl;
+      __syncthreads();
+      int slot = run + incl - c;
+      for (int wv = 0; wv < (int)(threadIdx.x >> 6); wv++) slot += s_wsum[wv];
+      while (bits) {
+        const int i = __ffsll((unsigned long long)bits) - 1;
+        bits &= bits - 1;
+        if (slot < kScanSlots) fill_candidate(d, D, q0 + i, out[slot]);
+        slot++;
+      }
+      run += s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+    }
+  }
+  if (threadIdx.x == 0) {
+    chunk_counts[blockIdx.x] = run;
+    if (run > kScanSlots) atomicOr(overflow, 1ull);
+  }
+}
+
 // slots -> file order: slot j of chunk b goes to chunk_off[b] + j (j < chunk_counts[b] <= kScanSlots)
 __global__ void k_scan_compact(const Candidate *__restrict__ slots, const int32_t *__restrict__ cnt,
                                const int64_t *__restrict__ off, int64_t nchunks, Candidate *__restrict__ out) {
@@ -343,8 +426,13 @@ hipError_t launch_scan_slots(const uint8_t *d, int64_t D, int32_t *cc, int64_t n
                              int64_t *overflow, hipStream_t s) {
   (void)hipMemsetAsync(overflow, 0, sizeof(int64_t), s);
   if (nchunks == 0) return hipSuccess;
+#if SBAM_SCAN_WIDE
+  hipLaunchKernelGGL(k_scan_slots_wide<SBAM_SCAN_WIDE>, dim3((unsigned)nchunks), dim3(kScanThreads), 0, s, d, D, cc,
+                     slots, reinterpret_cast<unsigned long long *>(overflow));
+#else
   hipLaunchKernelGGL(k_scan_slots, dim3((unsigned)nchunks), dim3(kScanThreads), 0, s, d, D, cc, slots,
                      reinterpret_cast<unsigned long long *>(overflow));
+#endif
   return hipGetLastError();
 }
 hipError_t launch_scan_compact(const Candidate *slots, const int32_t *cc, const int64_t *off, int64_t nchunks,

@@ -25,6 +25,7 @@ KERNELS = {"k_check_bits": "sbam::k_check_bits", "k_check<0, 0>": "sbam::k_check
            "k_check<1, 1>": "sbam::k_check<1, 1>", "k_check<1, 2>": "sbam::k_check<1, 2>",
            "k_chains": "sbam::k_chains",
            "k_scan_count": "sbam::k_scan_count", "k_scan_write": "sbam::k_scan_write", "k_scan_slots": "sbam::k_scan_slots",
+           "k_scan_slots_wide": "sbam::k_scan_slots_wide<32>",
            "k_scan_compact": "sbam::k_scan_compact",
            "k_record_counts": "sbam::k_record_counts", "k_eager": "sbam::k_eager"}
 
