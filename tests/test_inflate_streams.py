@@ -160,6 +160,34 @@ def test_scan_many_small_blocks(n_blocks):
         g.close()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("gap", [4099, 1021])
+def test_scan_fake_headers_every_alignment(gap):
+    """Stored blocks whose payloads hold a BGZF header pattern every `gap` bytes (Header.make's bytes 0-3 and
+    12-14), over > 2 MiB so that the fake candidates fall at every position of a lane's 32 and across the 1 MiB
+    scan chunks (gap 1021: > 512 candidates per chunk, the exact two-pass path).  MetadataStream follows BSIZE
+    from block 0, so the block table and bytes must equal the oracle's."""
+    import sbam
+    r = np.random.default_rng(gap)
+    fake = b"\x1f\x8b\x08\x04" + bytes(8) + b"BC\x02" + b"\x00\xff\x00"
+    datas = []
+    for i in range(40):
+        x = bytearray(r.integers(0, 256, int(r.integers(50000, 65000)), dtype=np.uint8).tobytes())
+        for o in range(int(r.integers(0, gap)), len(x) - len(fake), gap):
+            x[o:o + len(fake)] = fake
+        datas.append(bytes(x))
+    blocks = [bgzf_block(deflate(x, 0), len(x)) for x in datas]
+    data = b"".join(blocks) + EOF_BLOCK
+    assert len(data) > 2 << 20
+    assert oracle_result(data) == ("ok", b"".join(datas))
+    assert gpu_result(data) == ("ok", b"".join(datas))
+    g = sbam.BamFile(data, inflate=False)
+    try:
+        assert np.array_equal(g.blocks()[0], np.cumsum([0] + [len(b) for b in blocks[:-1]]))
+    finally:
+        g.close()
+
+
 # ---- a hand-placed fixed-Huffman stream: a round boundary of the wave decoder between a length and its distance --
 class _BitWriter:
     def __init__(self):
