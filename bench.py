@@ -366,6 +366,26 @@ def main():
             shard.f.check_eager_device(0, shard.f.uncompressed_size)
             em.append(shard.f.kernel_ms("check_eager_pass0"))
         eager_ms = float(np.median(em[1:]))
+    # loadReads: the chain proof is skipped when the eager pass's list found every link (no false-positive PASS0 site
+    # in the shard, as on the synthetic BAM); the same steps with the proof forced price a shard that has one
+    proof = None
+    if W == 1 and args.workload == "load-reads" and shard is not None:
+        os.environ["SBAM_FORCE_PROOF"] = "1"
+        try:
+            sync()
+            tp = time.perf_counter()
+            pms = []
+            for _ in range(max(2, args.steps // 2)):
+                _, m = step()
+                pms.append(m["records"])
+            sync()
+            pel = (time.perf_counter() - tp) / len(pms)
+        finally:
+            del os.environ["SBAM_FORCE_PROOF"]
+        proof = {"value": round(s.size / pel / 1e9, 3), "ms_per_step": round(pel * 1e3, 3),
+                 "records_ms": round(float(np.mean(pms)), 3), "steps": len(pms),
+                 "how": "the same step with SBAM_FORCE_PROOF=1: k_chain_proof reads every record's hop although the "
+                        "list pass found no missing link (what a shard with one false-positive PASS0 site costs)"}
     achieved = alg[dom] / (avg[dom] * 1e-3) / 1e9 if avg[dom] > 0 else 0.0
     traffic = measured_traffic(names[dom], args) if (args.read_len == 150 and W == 1) else None
 
@@ -467,6 +487,7 @@ def main():
                                                 "after the steps; not in the step"}} if eager_ms else {})),
             "hbm_copy_peak": cpk,
             "e2e_h2d": e2e,
+            **({"with_chain_proof": proof} if proof else {}),
             "cpu_baseline": cpu,
             "parity": parity,
         }

@@ -102,8 +102,10 @@ int sbam_load(sbam_ctx *ctx, const uint8_t *data, int64_t len, int64_t base_offs
  * ubytes uncompressed bytes and n_records records (0: leave the record-sized buffers alone), so that no later
  * sbam_load / stage reallocates: the buffers are grow-only, and growing one is a hipFree + hipMalloc of up to
  * tens of GB that synchronises the device (a streamed Spark task whose next split range is larger than any
- * before it).  Allocates nothing that is already large enough.  (No reference counterpart: the JVM channel has
- * no device memory; CanLoadBam.scala:281-334 re-opens a channel per split.) */
+ * before it).  Allocates nothing that is already large enough.  The resident compressed bytes and contig lengths
+ * are kept; when any stage buffer grows on a context that has already run a stage, every derived stage is
+ * dropped (as sbam_reset) and later queries re-run them.  (No reference counterpart: the JVM channel has no
+ * device memory; CanLoadBam.scala:281-334 re-opens a channel per split.) */
 int sbam_reserve(sbam_ctx *ctx, int64_t comp_bytes, int64_t n_blocks, int64_t ubytes, int64_t n_records);
 const sbam_error *sbam_last_error(const sbam_ctx *ctx);
 /* The path (Path.toString) that exception messages name, as the reference's HeaderSearchFailedException /

@@ -357,7 +357,15 @@ int sbam_reserve(sbam_ctx *c, int64_t comp_bytes, int64_t n_blocks, int64_t ubyt
   if (!c || comp_bytes < 0 || n_blocks < 0 || ubytes < 0 || n_records < 0) return SBAM_ERR_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (comp_bytes > c->D) {  // keep the resident bytes (sbam_load replaces them anyway)
+  // Any stage buffer that grows is a fresh allocation whose contents are gone, so a context that has already run a
+  // stage drops its stages (sbam_reset) when one grows: a later query re-runs them instead of reading uninitialised
+  // device memory.  The resident compressed bytes and the contig lengths are kept.
+  bool grew = false;
+  auto grow = [&](auto **p, size_t *cap, size_t n) {
+    grew |= *cap < std::max<size_t>(n, 1);
+    return ensure(p, cap, n);
+  };
+  if ((size_t)comp_bytes + kCompPad > c->comp_cap) {  // keep the resident bytes (sbam_load replaces them anyway)
     uint8_t *p = nullptr;
     HIPCHK(c, dalloc(&p, (size_t)comp_bytes + kCompPad));
     if (c->D + kCompPad > 0) HIPCHK(c, hipMemcpy(p, c->d_comp, (size_t)c->D + kCompPad, hipMemcpyDeviceToDevice));
@@ -366,38 +374,40 @@ int sbam_reserve(sbam_ctx *c, int64_t comp_bytes, int64_t n_blocks, int64_t ubyt
     c->comp_cap = (size_t)comp_bytes + kCompPad;
   }
   const int64_t nchunks = (comp_bytes + kScanChunk - 1) / kScanChunk;
-  HIPCHK(c, ensure(&c->d_cc, &c->cc_cap, nchunks));
-  HIPCHK(c, ensure(&c->d_coff, &c->coff_cap, nchunks));
-  HIPCHK(c, ensure(&c->d_slots, &c->slots_cap, (size_t)nchunks * kScanSlots));
+  HIPCHK(c, grow(&c->d_cc, &c->cc_cap, nchunks));
+  HIPCHK(c, grow(&c->d_coff, &c->coff_cap, nchunks));
+  HIPCHK(c, grow(&c->d_slots, &c->slots_cap, (size_t)nchunks * kScanSlots));
   // candidates: every block's header plus the rare false positives inside payloads
-  HIPCHK(c, ensure(&c->d_cand, &c->cand_cap, (size_t)(n_blocks + n_blocks / 8 + 1024)));
-  HIPCHK(c, ensure(&c->d_bstart, &c->bcap[0], n_blocks + 1));
-  HIPCHK(c, ensure(&c->d_bh, &c->bcap[1], n_blocks + 1));
-  HIPCHK(c, ensure(&c->d_bc, &c->bcap[2], n_blocks + 1));
-  HIPCHK(c, ensure(&c->d_bu, &c->bcap[3], n_blocks + 1));
-  HIPCHK(c, ensure(&c->d_buoff, &c->bcap[4], n_blocks + 1));
-  HIPCHK(c, ensure(&c->d_u, &c->u_cap, (size_t)ubytes + kStreamPad));
-  HIPCHK(c, ensure(&c->d_status, &c->status_cap, n_blocks));
-  HIPCHK(c, ensure(&c->d_found, &c->found_cap, n_blocks));
-  HIPCHK(c, ensure(&c->d_pool, &c->pool_cap, inflate_token_bytes(ubytes, n_blocks)));
+  HIPCHK(c, grow(&c->d_cand, &c->cand_cap, (size_t)(n_blocks + n_blocks / 8 + 1024)));
+  HIPCHK(c, grow(&c->d_bstart, &c->bcap[0], n_blocks + 1));
+  HIPCHK(c, grow(&c->d_bh, &c->bcap[1], n_blocks + 1));
+  HIPCHK(c, grow(&c->d_bc, &c->bcap[2], n_blocks + 1));
+  HIPCHK(c, grow(&c->d_bu, &c->bcap[3], n_blocks + 1));
+  HIPCHK(c, grow(&c->d_buoff, &c->bcap[4], n_blocks + 1));
+  HIPCHK(c, grow(&c->d_u, &c->u_cap, (size_t)ubytes + kStreamPad));
+  HIPCHK(c, grow(&c->d_status, &c->status_cap, n_blocks));
+  HIPCHK(c, grow(&c->d_found, &c->found_cap, n_blocks));
+  HIPCHK(c, grow(&c->d_pool, &c->pool_cap, inflate_token_bytes(ubytes, n_blocks)));
   if (inflate_arena_bytes(ubytes) > c->arena_cap) {
-    HIPCHK(c, ensure(&c->d_arena, &c->arena_cap, inflate_arena_bytes(ubytes) + 1024));
+    HIPCHK(c, grow(&c->d_arena, &c->arena_cap, inflate_arena_bytes(ubytes) + 1024));
     c->arena_cap -= 1024;
   }
-  HIPCHK(c, ensure(&c->d_tokbase, &c->tokbase_cap, n_blocks));
-  HIPCHK(c, ensure(&c->d_slow, &c->slow_cap, n_blocks));
+  HIPCHK(c, grow(&c->d_tokbase, &c->tokbase_cap, n_blocks));
+  HIPCHK(c, grow(&c->d_slow, &c->slow_cap, n_blocks));
+  grew |= (size_t)((ubytes + 63) / 64) + 1 > c->bitmap_cap;
   if (int rc = ensure_bitmap(c, 0, ubytes)) return rc;
-  HIPCHK(c, ensure(&c->d_tcnt, &c->tcnt_cap, (size_t)(4 * check_tiles(0, ubytes) + 8)));  // (x0 may add a tile)
+  HIPCHK(c, grow(&c->d_tcnt, &c->tcnt_cap, (size_t)(4 * check_tiles(0, ubytes) + 8)));  // (x0 may add a tile)
   if (n_records > 0) {  // the chain pass's PASS0 list (about one entry per record) and loadReads' offsets
     const size_t n = (size_t)(n_records + n_records / 8 + 4096);
-    HIPCHK(c, ensure(&c->d_plist, &c->plist_cap, n));
-    HIPCHK(c, ensure(&c->d_pfb, &c->pfb_cap, n));
-    HIPCHK(c, ensure(&c->d_pok, &c->pok_cap, n));
-    HIPCHK(c, ensure(&c->d_roff, &c->roff_cap, n));
+    HIPCHK(c, grow(&c->d_plist, &c->plist_cap, n));
+    HIPCHK(c, grow(&c->d_pfb, &c->pfb_cap, n));
+    HIPCHK(c, grow(&c->d_pok, &c->pok_cap, n));
+    HIPCHK(c, grow(&c->d_roff, &c->roff_cap, n));
     // loadReads' columns (sbam_load_records: an int64 column and ten int32 ones, 256-B aligned)
     const size_t stride = (n * 8 + 255) & ~(size_t)255, stride4 = (n * 4 + 255) & ~(size_t)255;
-    HIPCHK(c, ensure(&c->d_rcols, &c->rcols_cap, stride + 10 * stride4));
+    HIPCHK(c, grow(&c->d_rcols, &c->rcols_cap, stride + 10 * stride4));
   }
+  if (grew && (c->ncand >= 0 || c->nblocks >= 0 || c->L >= 0 || c->n_loaded >= 0)) return sbam_reset(c);
   return SBAM_OK;
 }
 
@@ -1057,8 +1067,12 @@ static int split_counts(sbam_ctx *c, bool try_bitmap, const std::vector<int64_t>
     int32_t *d_fail = reinterpret_cast<int32_t *>(c->d_small + 8);
     const int64_t xa = c->bm_x0 & ~(int64_t)63;
     HIPCHK(c, hipMemsetAsync(d_fail, 0, 4, c->stream));
-    HIPCHK(c, launch_chain_proof(c->d_u, c->L, c->d_bitmap, xa, X0, X1, d_fail, c->bm_list ? c->d_nfb : nullptr,
-                                 c->stream));
+    // SBAM_FORCE_PROOF=1 (measurement): run the proof even when the list pass found every link, as a bitmap with one
+    // false-positive PASS0 site anywhere in the range would (bench.py's loadReads line reports both)
+    const char *fp = std::getenv("SBAM_FORCE_PROOF");
+    const bool force = fp && *fp && *fp != '0';
+    HIPCHK(c, launch_chain_proof(c->d_u, c->L, c->d_bitmap, xa, X0, X1, d_fail,
+                                 (c->bm_list && !force) ? c->d_nfb : nullptr, c->stream));
     HIPCHK(c, launch_split_popcounts(c->d_bitmap, xa, c->d_sx, c->d_se, n, c->d_sn, d_fail, c->stream));
     int32_t fail = 1;
     HIPCHK(c, hipMemcpyAsync(&fail, d_fail, 4, hipMemcpyDeviceToHost, c->stream));

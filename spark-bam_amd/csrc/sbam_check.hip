@@ -434,8 +434,13 @@ __global__ __launch_bounds__(256) void k_p0_list(const unsigned long long *__res
     for (unsigned long long m = cw[j]; m; m &= m - 1) list[idx++] = x0a + ((w0 + j) << 6) + __builtin_ctzll(m);
 }
 
+// ok[i]: p_i's record hops to p_(i+1) past its name and CIGAR.  The last entry has no successor in the list: its
+// link holds when its hop leaves the checked range [x0, x1) without passing the stream end, which is what the chain
+// proof (sbam_records.hip) needs of the last set bit when it skips on "no missing link" (for R = 1 no fallback walk
+// checks that hop).
 __global__ __launch_bounds__(256) void k_p0_links(StreamView sv, const int64_t *__restrict__ list,
-                                                  const int64_t *__restrict__ n_ptr, uint8_t *__restrict__ ok) {
+                                                  const int64_t *__restrict__ n_ptr, int64_t x1,
+                                                  uint8_t *__restrict__ ok) {
   const int64_t n = *n_ptr;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t p = list[i];
@@ -444,12 +449,13 @@ __global__ __launch_bounds__(256) void k_p0_links(StreamView sv, const int64_t *
     const int32_t nc = (int32_t)((uint32_t)sv.u[p + 16] | ((uint32_t)sv.u[p + 17] << 8));
     const int64_t c_end = p + 36 + (lrn >= 2 ? lrn : 0) + 4 * (int64_t)nc;
     const int64_t nxt = p + 4 + (int64_t)bs;
-    ok[i] = (i + 1 < n && list[i + 1] == nxt && nxt > c_end) ? 1 : 0;
+    const bool link = i + 1 < n ? list[i + 1] == nxt : (nxt >= x1 && nxt <= sv.L);
+    ok[i] = (link && nxt > c_end) ? 1 : 0;
   }
 }
 
 // Success when the R-1 links from p_i hold; every other PASS0 position goes to the fallback list.  n_fb[1] counts
-// the missing links between consecutive list entries: with none (and no failing fallback, n_fb[2]) the success
+// the missing links between consecutive list entries and a last entry whose hop stays inside [x0, x1): with none (and no failing fallback, n_fb[2]) the success
 // bitmap IS the list and every set bit hops to the next one — the chain proof of the split records
 // (sbam_records.hip) then holds without another pass over the records.
 __global__ __launch_bounds__(256) void k_p0_fast(const int64_t *__restrict__ list, const int64_t *__restrict__ n_ptr,
@@ -462,7 +468,7 @@ __global__ __launch_bounds__(256) void k_p0_fast(const int64_t *__restrict__ lis
     for (int k = 0; succ && k < R - 1; k++) succ = ok[i + k] != 0;
     if (succ) n_succ++;
     else fb[atomicAdd(n_fb, 1ull)] = list[i];
-    n_gap += (i + 1 < n && !ok[i]) ? 1u : 0u;
+    n_gap += !ok[i] ? 1u : 0u;
   }
   if (__ballot(n_gap != 0)) {
     n_gap = wave_sum(n_gap);
@@ -500,7 +506,7 @@ __global__ __launch_bounds__(256) void k_p0_fast16(const int64_t *__restrict__ l
         const bool succ = i + (R - 1) <= n - 1 && ((m >> j) & need) == need;
         if (succ) n_succ++;
         else fb[atomicAdd(n_fb, 1ull)] = list[i];
-        n_gap += (i + 1 < n && !((m >> j) & 1u)) ? 1u : 0u;
+        n_gap += !((m >> j) & 1u) ? 1u : 0u;
       }
     }
   }
@@ -1733,7 +1739,7 @@ hipError_t launch_chain_list_run(StreamView sv, int64_t x0, int64_t x1, int32_t 
   if (nch <= 0) return hipSuccess;
   const int64_t *n_ptr = cs.chunk_off + nch;
   hipLaunchKernelGGL(k_p0_list, dim3((unsigned)nch), dim3(256), 0, s, bitmap, nwords, x0a, cs.chunk_off, cs.list);
-  hipLaunchKernelGGL(k_p0_links, dim3(4096), dim3(256), 0, s, sv, cs.list, n_ptr, cs.ok);
+  hipLaunchKernelGGL(k_p0_links, dim3(4096), dim3(256), 0, s, sv, cs.list, n_ptr, x1, cs.ok);
   (void)hipMemsetAsync(cs.n_fb, 0, 3 * sizeof(unsigned long long), s);  // fallbacks, missing links, failed fallbacks
   if (R >= 2 && R <= 10)
     hipLaunchKernelGGL(k_p0_fast16, dim3(1024), dim3(256), 0, s, cs.list, n_ptr, cs.ok, (int)R, cd, cs.fb, cs.n_fb);

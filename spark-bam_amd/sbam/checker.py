@@ -8,11 +8,18 @@ source (the channel) and nothing about the partition; the first `apply(pos)` in 
 ONE bulk GPU call over that block and the blocks after it (a window of compressed bytes), and caches their calls; every
 later `apply` in those blocks is a bit (or word) lookup — the shape of the reference's own bulk-precomputed
 `indexed.Checker` (check/.../check/indexed/Checker.scala:12-27).  A window whose checked chains run past its bytes
-(HALO: long records) doubles and retries.  INTEGRATION.md shows the same class on the JVM (Panama)."""
+(HALO: long records) doubles and retries.  INTEGRATION.md shows the same class on the JVM (Panama).
+
+The eager kind is also the reference's `ReadStartFinder` (check/.../check/ReadStartFinder.scala:5-11; eager.Checker
+mixes it in, eager/Checker.scala:18-22, 128-162): `next_read_start(pos)` walks the uncompressed positions from `pos`
+over the cached calls, block after block (filling windows as it goes), for at most `max_read_size` positions — what
+check-blocks' `callPartition` asks of both of its checkers (cli/.../check/blocks/CheckBlocks.scala:37-56).
+`IndexedChecker` is the other side of that comparison: indexed.Checker over a `.records` set."""
 from __future__ import annotations
 
 from collections import OrderedDict
-from typing import Callable, Dict, Optional, Sequence
+import bisect
+from typing import Callable, Dict, Iterable, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -37,6 +44,7 @@ class LazyBlockChecker:
         self.R, self.window, self.device, self.kind, self.keep = reads_to_check, int(window), device, kind, keep
         self.windows: "OrderedDict[int, Dict[int, np.ndarray]]" = OrderedDict()  # window start → {block start → calls}
         self.cache: Dict[int, np.ndarray] = {}  # block start → calls at offsets 0 .. usize-1 (the kept windows)
+        self.next_block: Dict[int, int] = {}     # block start → the next block's start (start + compressed size)
         self.bulk_calls = 0                      # GPU windows computed (one per cache miss, plus HALO retries)
         self.f: Optional[sbam.BamFile] = None
 
@@ -76,7 +84,9 @@ class LazyBlockChecker:
             while len(self.windows) > self.keep:
                 for k in self.windows.popitem(last=False)[1]:
                     self.cache.pop(k, None)
+                    self.next_block.pop(k, None)
             self.cache.update(blocks)
+            self.next_block.update({int(st[b]): int(st[b]) + int(cs[b]) for b in range(nb)})
             return
 
     def apply(self, pos: sbam.Pos):
@@ -89,6 +99,54 @@ class LazyBlockChecker:
 
     __call__ = apply
 
+    def _calls(self, block_pos: int, first: bool) -> Optional[np.ndarray]:
+        """The calls of the block at block_pos; None when the block chain (followed from an earlier block) has no
+        further block with data there: the EOF marker, an empty block or the file's end (MetadataStream stops)."""
+        calls = self.cache.get(block_pos)
+        if calls is None:
+            try:
+                self._fill(block_pos)
+            except sbam.SbamError:
+                if first:
+                    raise
+                return None
+            calls = self.cache[block_pos]
+        return calls
+
+    def next_read_start_with_delta(self, start: sbam.Pos,
+                                   max_read_size: int = sbam.MAX_READ_SIZE) -> Optional[Tuple[sbam.Pos, int]]:
+        """eager.Checker.nextReadStartWithDelta (eager/Checker.scala:133-162): the first position at or after `start`
+        whose call is true, with the number of positions passed over; None after `max_read_size` positions, or when
+        the uncompressed stream ends (the end of the file, or an empty block: MetadataStream stops there)."""
+        if self.kind != "eager":
+            raise TypeError("ReadStartFinder is eager.Checker's (full.Checker has no nextReadStart)")
+        bp, off, idx = int(start.block_pos), int(start.offset), 0
+        while idx < max_read_size:
+            if bp >= self.file_size:
+                return None
+            calls = self._calls(bp, first=idx == 0 and bp == int(start.block_pos))
+            if calls is None or calls.size == 0:
+                return None
+            n = int(calls.size)
+            if off >= n:  # Pos(block, usize) is the next block's start (UncompressedBytes' curPos)
+                off -= n
+                bp = self.next_block[bp]
+                continue
+            seg = calls[off: off + min(n - off, max_read_size - idx)]
+            hit = np.flatnonzero(seg)
+            if hit.size:
+                return sbam.Pos(bp, off + int(hit[0])), idx + int(hit[0])
+            idx += seg.size
+            off = n
+        return None
+
+    def next_read_start(self, start: sbam.Pos, max_read_size: int = sbam.MAX_READ_SIZE) -> Optional[sbam.Pos]:
+        """ReadStartFinder.nextReadStart (ReadStartFinder.scala:5-11; eager/Checker.scala:127-131)."""
+        r = self.next_read_start_with_delta(start, max_read_size)
+        return None if r is None else r[0]
+
+    nextReadStart = next_read_start
+
     def close(self):
         """The partition is done (CallPartition's .finish(close)): release the device context."""
         if self.f is not None:
@@ -100,6 +158,37 @@ class LazyBlockChecker:
 
     def __exit__(self, *a):
         self.close()
+
+
+class IndexedChecker:
+    """indexed.Checker (check/src/main/scala/org/hammerlab/bam/check/indexed/Checker.scala:12-27): the calls of a
+    known set of record starts (a `.records` sidecar) — apply(pos) is membership, nextReadStart the first member at or
+    after `pos`.  It is the truth side of check-blocks' comparison (CheckBlocks.scala:80-91)."""
+
+    def __init__(self, read_positions: Iterable[sbam.Pos]):
+        self.positions = sorted(set(read_positions))
+        self._set = set(self.positions)
+
+    @classmethod
+    def from_records_file(cls, path: str) -> "IndexedChecker":
+        """A `.records` sidecar: one `blockPos,offset` line per record (IndexRecords.scala:36-90)."""
+        out = []
+        for ln in open(path):
+            if ln.strip():
+                b, o = ln.split(",")
+                out.append(sbam.Pos(int(b), int(o)))
+        return cls(out)
+
+    def apply(self, pos: sbam.Pos) -> bool:
+        return pos in self._set
+
+    __call__ = apply
+
+    def next_read_start(self, start: sbam.Pos, max_read_size: int = sbam.MAX_READ_SIZE) -> Optional[sbam.Pos]:
+        i = bisect.bisect_left(self.positions, start)
+        return self.positions[i] if i < len(self.positions) else None
+
+    nextReadStart = next_read_start
 
 
 def make_checker(contig_lengths: Sequence[int], reads_to_check: int = sbam.READS_TO_CHECK, kind: str = "eager",

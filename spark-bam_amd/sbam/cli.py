@@ -29,7 +29,7 @@ import os
 import sys
 import time
 from dataclasses import dataclass
-from typing import List, Optional, Sequence, Tuple
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -564,19 +564,30 @@ def check_blocks_lines(f: sbam.BamFile, truth_offsets: np.ndarray, limit: int,
     L = f.uncompressed_size
     eager = np.flatnonzero(f.check_eager(0, L, reads_to_check)).astype(np.int64)
     truth = np.sort(np.asarray(truth_offsets, np.int64))
+    by_start = {int(st[b]): int(uo[b]) for b in range(st.size)}
 
-    def pos(x):
-        return None if x is None else f.pos_of(x)
+    def finder(offs):
+        def next_read_start(p: sbam.Pos) -> Optional[sbam.Pos]:
+            x = _next_start(offs, by_start[p.block_pos] + p.offset)
+            return None if x is None else f.pos_of(x)
+        return next_read_start
 
+    blocks = [(int(st[b]), int(cs[b])) for b in range(st.size)]
+    return check_blocks_report(blocks, finder(eager), finder(truth), f.file_size, limit)
+
+
+def check_blocks_report(blocks: Sequence[Tuple[int, int]], next1: Callable[[sbam.Pos], Optional[sbam.Pos]],
+                        next2: Callable[[sbam.Pos], Optional[sbam.Pos]], size: int, limit: int) -> List[str]:
+    """CheckBlocks.callPartition + run (CheckBlocks.scala:37-190) over (start, compressedSize) blocks in file order and
+    two ReadStartFinders' nextReadStart (e.g. sbam.checker.LazyBlockChecker and IndexedChecker): the report text."""
     bad, offs = [], {}
-    for b in range(st.size):
-        p1, p2 = pos(_next_start(eager, int(uo[b]))), pos(_next_start(truth, int(uo[b])))
-        off = p1.offset if p1 is not None and p1.block_pos == int(st[b]) else None
+    for b, (start, _) in enumerate(blocks):
+        p1, p2 = next1(sbam.Pos(start, 0)), next2(sbam.Pos(start, 0))
+        off = p1.offset if p1 is not None and p1.block_pos == start else None
         offs[off] = offs.get(off, 0) + 1
         if (str(p1) if p1 else None) != (str(p2) if p2 else None):
-            bad.append((int(st[b]), p1, p2, int(cs[b - 1]) if b > 0 else 1))
-    size = f.file_size
-    n_blocks = int(st.size)
+            bad.append((start, p1, p2, blocks[b - 1][1] if b > 0 else 1))
+    n_blocks = len(blocks)
     out: List[str] = []
 
     def offsets_info():

@@ -268,39 +268,192 @@ def gather_results(res: ShardResult, plans: Sequence[ShardPlan], device=None) ->
 # ---- file-level driver ----------------------------------------------------------------------------------------
 
 # HBM per compressed byte of one loaded range (DESIGN.md §Data layout): the compressed bytes, the uncompressed
-# stream (r per byte, r = uncompressed / compressed), the decoder's token regions (2 r: u16 per uncompressed byte,
-# reserved whole), the success bitmap (r / 8), plus block tables, candidates and the checker's lists (< 0.05).
-def hbm_bytes_per_compressed_byte(ratio: float) -> float:
+# stream (r per byte, r = uncompressed / compressed), the decoder's main token regions (r: 1 B per uncompressed byte),
+# the success bitmap (r / 8), the token arena, plus block tables, candidates and the checker's lists (< 0.05).
+# The arena's default is 1/16 B per uncompressed byte, but a block whose tokens outgrow its main region (more than
+# (ISIZE + 16) / 2 tokens: stored blocks, Huffman-only or RLE streams — fewer than 2 output bytes per token) takes
+# 2 B per uncompressed byte there (sbam_inflate grows the arena to what the blocks asked for and decodes again).  The
+# compression ratio does not tell such blocks apart (Huffman-only over a 4-letter alphabet compresses 4:1), so
+# bgzf_sample_stats counts the DEFLATE tokens of a few sampled blocks.
+
+
+def hbm_bytes_per_compressed_byte(ratio: float, arena_frac: float = 0.0) -> float:
     """Device bytes a loaded range needs per compressed byte at compression ratio `ratio`: the compressed bytes, and
-    per uncompressed byte the stream (1), the main token regions (1), the success bitmap (1/8) and the default token
-    arena (1/16); block tables and scratch ~0.05."""
-    return 1.0 + ratio * (1.0 + 1.0 + 0.125 + 0.0625) + 0.05
+    per uncompressed byte the stream (1), the main token regions (1), the success bitmap (1/8) and the token arena
+    (the default 1/16, or 2 B per byte of the `arena_frac` of the output in blocks that need it, whichever is more);
+    block tables and scratch ~0.05."""
+    arena = max(0.0625, 2.0 * arena_frac * 1.125)
+    return 1.0 + ratio * (1.0 + 1.0 + 0.125 + arena) + 0.05
 
 
-def bgzf_ratio(source: Callable[..., np.ndarray], size: int, sample: int = 8 << 20) -> float:
-    """Uncompressed / compressed bytes over the BGZF blocks of the first `sample` bytes (the block chain from the
-    first header: BSIZE at +16, ISIZE in the block's last 4 bytes — Header.scala, the footer); 3.0 when nothing
-    parses."""
-    buf = source(0, min(size, sample))
-    raw = buf.tobytes()
-    pos = 0  # the first BGZF header (a range may start inside a block): magic 1f 8b 08 04, 'BC' at +12
+def _first_header(raw: bytes) -> int:
+    """Offset of the first BGZF header (magic 1f 8b 08 04, 'BC' at +12) in `raw`, or -1 (a range may start inside
+    a block)."""
+    pos = 0
     while True:
         pos = raw.find(b"\x1f\x8b\x08\x04", pos)
         if pos < 0 or raw[pos + 12:pos + 14] == b"BC":
-            break
+            return pos
         pos += 1
+
+
+_CL_ORDER = (16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15)
+_LEN_EXTRA = [0] * 8 + [k // 4 - 1 for k in range(8, 28)] + [0]
+_DIST_EXTRA = [0] * 4 + [k // 2 - 1 for k in range(4, 30)]
+
+
+def _huff_table(lengths):
+    """15-bit lookup table of a canonical code (stream bits LSB first): entry = symbol << 4 | length (0 = no code)."""
+    tab = [0] * 32768
+    code, nxt, cnt = 0, [0] * 16, [0] * 16
+    for l in lengths:
+        cnt[l] += 1
+    cnt[0] = 0
+    for l in range(1, 16):
+        code = (code + cnt[l - 1]) << 1
+        nxt[l] = code
+    for sym, l in enumerate(lengths):
+        if l:
+            c = nxt[l]
+            nxt[l] += 1
+            r = int(format(c, f"0{l}b")[::-1], 2)
+            e = (sym << 4) | l
+            for j in range(r, 32768, 1 << l):
+                tab[j] = e
+    return tab
+
+
+def deflate_token_count(payload: bytes, limit: int = 1 << 20) -> int:
+    """Tokens (literals + lengths + distances, the decoder's u16 stream) of a raw DEFLATE stream, or -1 when it does not
+    parse; stops after `limit` output bytes.  (RFC 1951; used only to budget HBM for the token arena.)"""
+    n = len(payload)
+    pos = 0          # next byte to enter the bit buffer
+    bb = bc = 0      # bit buffer (LSB first) and its count
+
+    def need(k):
+        nonlocal pos, bb, bc
+        while bc < k:
+            bb |= (payload[pos] if pos < n else 0) << bc
+            pos += 1
+            bc += 8
+
+    def bits(k):
+        nonlocal bb, bc
+        need(k)
+        v = bb & ((1 << k) - 1)
+        bb >>= k
+        bc -= k
+        return v
+
+    def sym(tab):
+        nonlocal bb, bc
+        need(15)
+        e = tab[bb & 32767]
+        if not e:
+            raise ValueError
+        bb >>= e & 15
+        bc -= e & 15
+        return e >> 4
+
+    tokens = out = 0
+    try:
+        while out < limit:
+            fin, typ = bits(1), bits(2)
+            if typ == 0:
+                bb >>= bc & 7
+                bc -= bc & 7
+                ln = bits(16)
+                bits(16)
+                tokens += ln
+                out += ln
+                skip = max(0, ln - bc // 8)
+                bb = bc = 0 if skip else bb
+                pos += skip
+            elif typ in (1, 2):
+                if typ == 1:
+                    ll = [8] * 144 + [9] * 112 + [7] * 24 + [8] * 8
+                    dl = [5] * 30
+                else:
+                    hlit, hdist, hclen = bits(5) + 257, bits(5) + 1, bits(4) + 4
+                    cl = [0] * 19
+                    for i in range(hclen):
+                        cl[_CL_ORDER[i]] = bits(3)
+                    ctab = _huff_table(cl)
+                    lens = []
+                    while len(lens) < hlit + hdist:
+                        s_ = sym(ctab)
+                        if s_ < 16:
+                            lens.append(s_)
+                        elif s_ == 16:
+                            lens += [lens[-1]] * (3 + bits(2))
+                        else:
+                            lens += [0] * ((3 + bits(3)) if s_ == 17 else (11 + bits(7)))
+                    ll, dl = lens[:hlit], lens[hlit:hlit + hdist]
+                ltab, dtab = _huff_table(ll), _huff_table(dl)
+                while True:
+                    s_ = sym(ltab)
+                    if s_ < 256:
+                        tokens += 1
+                        out += 1
+                    elif s_ == 256:
+                        break
+                    else:
+                        k = s_ - 257
+                        base = (k + 3) if k < 8 else 258 if k == 28 else (((4 | (k & 3)) << _LEN_EXTRA[k]) + 3)
+                        out += base + bits(_LEN_EXTRA[k])
+                        d = sym(dtab)
+                        bits(_DIST_EXTRA[d])
+                        tokens += 2
+                    if out >= limit:
+                        break
+            else:
+                return -1
+            if fin:
+                break
+    except (ValueError, IndexError):
+        return -1
+    return tokens
+
+
+def bgzf_sample_stats(source: Callable[..., np.ndarray], size: int, sample: int = 8 << 20,
+                      token_blocks: int = 12) -> Tuple[float, float]:
+    """(uncompressed / compressed, share of the uncompressed bytes in blocks whose tokens outgrow the main token
+    region) over the BGZF blocks of the first `sample` bytes (the block chain from the first header: BSIZE at +16,
+    ISIZE in the block's last 4 bytes — Header.scala, the footer); the token share from `token_blocks` blocks spread
+    over the sample (a block that does not parse counts as an arena block); (3.0, 0.0) when nothing parses."""
+    buf = source(0, min(size, sample))
+    raw = buf.tobytes()
+    pos = _first_header(raw)
     if pos < 0:
-        return 3.0
+        return 3.0, 0.0
     comp = unc = 0
-    while pos + 18 <= buf.size and buf[pos] == 0x1F and buf[pos + 1] == 0x8B:
-        bsize = int(buf[pos + 16]) | (int(buf[pos + 17]) << 8)
+    blocks = []
+    while pos + 18 <= len(raw) and raw[pos] == 0x1F and raw[pos + 1] == 0x8B:
+        bsize = raw[pos + 16] | (raw[pos + 17] << 8)
         end = pos + bsize + 1
-        if end > buf.size:
+        if end > len(raw):
             break
-        unc += int.from_bytes(buf[end - 4:end].tobytes(), "little")
+        isz = int.from_bytes(raw[end - 4:end], "little")
+        unc += isz
         comp += bsize + 1
+        blocks.append((pos, end, isz))
         pos = end
-    return unc / comp if comp and unc else 3.0
+    if not (comp and unc):
+        return 3.0, 0.0
+    picks = sorted({int(i) for i in np.linspace(0, len(blocks) - 1, min(token_blocks, len(blocks)))})
+    tot = big = 0
+    for i in picks:
+        st, end, isz = blocks[i]
+        xlen = raw[st + 10] | (raw[st + 11] << 8)
+        t = deflate_token_count(raw[st + 12 + xlen:end - 8], isz)
+        tot += isz
+        big += isz if (t < 0 or t > (isz + 16) // 2) else 0
+    return unc / comp, (big / tot if tot else 0.0)
+
+
+def bgzf_ratio(source: Callable[..., np.ndarray], size: int, sample: int = 8 << 20) -> float:
+    """Uncompressed / compressed bytes over the BGZF blocks of the first `sample` bytes (bgzf_sample_stats)."""
+    return bgzf_sample_stats(source, size, sample)[0]
 
 
 def bgzf_buffer_stats(buf: np.ndarray) -> Tuple[float, float]:
@@ -328,8 +481,10 @@ def bgzf_buffer_stats(buf: np.ndarray) -> Tuple[float, float]:
 def auto_windows(size: int, source: Callable[..., np.ndarray], free_bytes: int, contexts: int = 2,
                  headroom: float = 0.8) -> int:
     """Windows for a `size`-byte range so that `contexts` loaded windows (WindowPipe keeps two) fit in `headroom` of
-    `free_bytes` of HBM, from the file's measured compression ratio (with 10 % margin)."""
-    per_byte = hbm_bytes_per_compressed_byte(1.1 * bgzf_ratio(source, size))
+    `free_bytes` of HBM, from the file's measured compression ratio (with 10 % margin) and the share of its output in
+    low-ratio blocks, whose tokens may take the arena at 2 B per byte (stored / Huffman-only inputs)."""
+    ratio, arena_frac = bgzf_sample_stats(source, size)
+    per_byte = hbm_bytes_per_compressed_byte(1.1 * ratio, arena_frac)
     need = size * per_byte * contexts
     return max(1, int(np.ceil(need / (headroom * free_bytes))))
 

@@ -127,6 +127,39 @@ def test_reserve_then_larger_window_gpu():
 
 
 @pytest.mark.gpu
+def test_reserve_after_run_drops_stages_gpu():
+    """sbam_reserve on a context that has already scanned, inflated and checked, growing its buffers,
+    must not leave stale stage state over fresh (uninitialised) allocations: the C context drops its stages (a
+    stream query is then SBAM_ERR_STATE) and the Python wrapper re-runs them, so the calls equal a fresh context's."""
+    import numpy as np
+    import sbam
+    from conftest import fixture_bytes
+    a = fixture_bytes("2.bam")
+    with sbam.BamFile(a) as fresh:
+        want_calls = fresh.check_eager(0, fresh.uncompressed_size)
+        want_counts = fresh.check_full_counts(0, fresh.uncompressed_size)
+        L_, nb = int(fresh.uncompressed_size), int(fresh.n_blocks)
+    L = sbam.load_library()
+    with sbam.BamFile(a) as f:
+        f.check_full_counts(0, L_)
+        # raw ABI: the grown context reports that inflate has to run again
+        assert L.sbam_reserve(f.ctx, 8 * len(a), 8 * nb, 8 * L_, 0) == sbam.SBAM_OK
+        assert L.sbam_read_uncompressed(f.ctx, 0, 0, None) == sbam.ERR_STATE
+        f.n_blocks = f._scan()
+        f.inflate()
+        assert np.array_equal(f.check_eager(0, L_), want_calls)
+        # the wrapper: reserve larger again, then query without re-running by hand
+        f.reserve(16 * len(a), 16 * nb, 16 * L_, 1 << 16)
+        assert f.uncompressed_size == L_
+        c = f.check_full_counts(0, L_)
+        assert np.array_equal(c.totals, want_counts.totals) and c.n_success == want_counts.n_success
+        assert np.array_equal(f.check_eager(0, L_), want_calls)
+        # nothing grows: the stages stay
+        f.reserve(len(a), nb, L_, 0)
+        assert L.sbam_read_uncompressed(f.ctx, 0, 0, None) == sbam.SBAM_OK
+
+
+@pytest.mark.gpu
 def test_load_window_gpu():
     """sbam_load: a context re-filled with another file (and back) gives the same blocks, stream and checker
     calls as a fresh sbam_open of that file, with its allocations reused."""

@@ -108,3 +108,48 @@ def test_check_blocks_report(bam, golden, tmp_path):
     out = tmp_path / "out.txt"
     assert cli.main(["check-blocks", "-s", str(path), str(out)]) == 0
     assert out.read_text() == _golden(golden)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bam,golden,window", [("1.bam", "1.bam-s", 100 * 1024), ("2.bam", "2.bam", 64 * 1024),
+                                               ("1.block-aligned.bam", "1.block-aligned.bam", 256 * 1024)])
+def test_check_blocks_through_read_start_finders(bam, golden, window, tmp_path):
+    """check-blocks' callPartition (CheckBlocks.scala:37-56) run through the drop-in ReadStartFinders: the GPU-backed
+    LazyBlockChecker's nextReadStart (eager.Checker, eager/Checker.scala:127-162) against IndexedChecker's
+    (indexed.Checker over the `.records` set), block by block with small windows so the walks cross windows; the
+    report equals the reference's CheckBlocksTest text, and nextReadStart at sampled positions equals the truth's."""
+    from sbam import Pos, cli, dist as sdist
+    from sbam.checker import IndexedChecker, LazyBlockChecker
+    path = tmp_path / bam
+    shutil.copy(os.path.join(FIXTURES, bam), path)
+    rec = os.path.join(FIXTURES, bam + ".records")
+    if not os.path.exists(rec):
+        rec = str(path) + ".records"
+        assert cli.main(["index-records", str(path), rec]) == 0
+    import sbam
+    with sbam.BamFile(open(path, "rb").read()) as f:
+        st, cs, us, uo = f.blocks()
+        lens = f.contig_lengths
+    blocks = [(int(a), int(b)) for a, b in zip(st, cs)]  # (Blocks(): the BGZF block metadata, file order)
+    truth = IndexedChecker.from_records_file(rec)
+    eager = LazyBlockChecker(*sdist.file_source(str(path)), lens, window=window)
+    try:
+        text = "\n".join(cli.check_blocks_report(blocks, eager.next_read_start, truth.next_read_start,
+                                                 os.path.getsize(path), 10)) + "\n"
+        assert text == _golden(golden)
+        assert eager.bulk_calls > 1
+        rng = np.random.default_rng(11)
+        for b in rng.choice(len(blocks), min(len(blocks), 12), replace=False):
+            start, _ = blocks[int(b)]
+            for o in np.sort(rng.integers(0, int(us[int(b)]), 8)):
+                p = Pos(start, int(o))
+                assert eager.next_read_start(p) == truth.next_read_start(p), (bam, p)
+                got = eager.next_read_start_with_delta(p)
+                if got is not None:  # the delta counts positions (bytes of the uncompressed stream) passed over
+                    q, d = got
+                    assert eager.next_read_start(p, max_read_size=d) is None
+                    assert eager.next_read_start(p, max_read_size=d + 1) == q
+        last = blocks[-1][0]
+        assert eager.next_read_start(Pos(last, int(us[-1]) - 1)) == truth.next_read_start(Pos(last, int(us[-1]) - 1))
+    finally:
+        eager.close()

@@ -301,6 +301,49 @@ def test_hbm_budget_and_auto_windows():
     assert abs(sdist.bgzf_ratio(lambda lo, hi: src(lo + 1000, hi + 1000), size - 1000) - r) < 0.05
     per = sdist.hbm_bytes_per_compressed_byte(1.1 * r)
     assert abs(per - (1 + 1.1 * r * 2.1875 + 0.05)) < 1e-9
+    assert sdist.bgzf_sample_stats(src, size)[1] < 0.05  # zlib-6 BAM blocks: the arena's default share
     need = size * per * 2
     assert sdist.auto_windows(size, src, int(need / 0.8) + 1) == 1
     assert sdist.auto_windows(size, src, int(need / 0.8 / 3) + 1) == 3
+
+
+def _bgzf_block(payload: bytes, level: int, strategy: int = 0) -> bytes:
+    """One BGZF block (RFC 1952 member with the BC extra field) of `payload`, raw-deflated at `level`."""
+    import struct
+    import zlib
+    co = zlib.compressobj(level, zlib.DEFLATED, -15, 9, strategy)
+    data = co.compress(payload) + co.flush()
+    bsize = 18 + len(data) + 8 - 1
+    hdr = b"\x1f\x8b\x08\x04" + b"\x00" * 4 + b"\x00\xff" + struct.pack("<HBBHH", 6, 66, 67, 2, bsize)
+    return hdr + data + struct.pack("<II", zlib.crc32(payload), len(payload))
+
+
+def test_auto_windows_budgets_arena_for_stored_blocks():
+    """stored and Huffman-only blocks need 2 B of token arena per uncompressed byte, so auto_windows
+    budgets them (bgzf_sample_stats' low-ratio share) instead of the 1/16 default, and picks more windows than the
+    same ratio at the default would."""
+    import zlib
+    from sbam import dist as sdist
+    rng = np.random.default_rng(5)
+    raw = rng.integers(0, 4, 60000, dtype=np.uint8).tobytes()
+    stored = b"".join(_bgzf_block(raw, 0) for _ in range(40))
+    huff = b"".join(_bgzf_block(raw, 6, zlib.Z_HUFFMAN_ONLY) for _ in range(40))
+    for blob in (stored, huff):
+        buf = np.frombuffer(blob, np.uint8)
+        src = (lambda b: lambda lo, hi: b[lo:hi])(buf)
+        r, frac = sdist.bgzf_sample_stats(src, buf.size)
+        assert frac == 1.0
+        per = sdist.hbm_bytes_per_compressed_byte(1.1 * r, frac)
+        assert per > sdist.hbm_bytes_per_compressed_byte(1.1 * r) + 2.0 * 1.1 * r
+        free = int(buf.size * per * 2 / 0.8 / 2) + 1  # room for half of what the worst case needs
+        assert sdist.auto_windows(buf.size, src, free) == 2
+    # the token counter: one token per byte for stored and Huffman-only streams; zlib-6 matches take two tokens each
+    import zlib as z
+    for level, strat in ((0, 0), (6, z.Z_HUFFMAN_ONLY)):
+        co = z.compressobj(level, z.DEFLATED, -15, 9, strat)
+        assert sdist.deflate_token_count(co.compress(raw) + co.flush()) == len(raw)
+    text = b"".join(b"read%07d\tACGTTGCA\n" % i for i in range(3000))
+    co = z.compressobj(6, z.DEFLATED, -15, 8, 0)
+    t = sdist.deflate_token_count(co.compress(text) + co.flush())
+    assert 0 < t < len(text) // 2 and t % 1 == 0
+    assert sdist.deflate_token_count(b"\xff\xff\xff") == -1  # block type 3
