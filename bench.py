@@ -483,7 +483,7 @@ def main():
                                         "achieved": round((U + U // 8) / (eager_ms * 1e-3) / 1e9, 2),
                                         "frac": round((U + U // 8) / (eager_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                         "algorithmic_bytes": U + U // 8, "avg_launch_ms": round(eager_ms, 3),
-                                        "note": "compute-splits' eager checker (k_eager + boundary tiles), timed "
+                                        "note": "compute-splits' eager checker (k_eager_wave + boundary tiles), timed "
                                                 "after the steps; not in the step"}} if eager_ms else {})),
             "hbm_copy_peak": cpk,
             "e2e_h2d": e2e,

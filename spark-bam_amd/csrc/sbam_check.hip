@@ -1386,145 +1386,164 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bi
     if (s_pair[i]) atomicAdd(&cd.pair[i], (unsigned long long)s_pair[i]);
 }
 
-// ---- eager record-0 pass over interior tiles, with a prefilter -------------------------------------------------
+// ---- eager record-0 pass over interior tiles, one wave per tile, with a prefilter ---------------------------------
 // eager.Checker fails a position at its first failing check, and the first checks are the two reference indices
 // (refIdx, nextRefIdx in [-1, n_ref): PosChecker.scala:43-63, eager/Checker.scala:24-126).  So every position is
-// first tested on those two fields alone (two funnel shifts and two compares per position); only the survivors —
-// true record starts and the few positions whose indices happen to be small — are queued per wave and checked in
-// full (eager_pass_direct, all 64 lanes on queued positions).  Same PASS0 bitmap as k_check<MODE_EAGER, 1>.
-constexpr int kEagerQ = 2048;      // workgroup queue of survivors (a tile's are queued in rounds of this many)
-constexpr int kEagerLens = 1024;   // contig lengths in LDS (more: read from HBM) — keeps 8 workgroups per CU
-// eager.Checker at an interior position whose indices passed the prefilter, straight from the staged bytes (no
-// op-class / name-character bitmaps: survivors are few, and a true record's name and CIGAR are short).  Same
-// pass/fail as check_first<true, true>.
-SB_DEV bool eager_pass_direct(const uint8_t *win, const StreamView &sv, const int32_t *lensL, int64_t x, int rel,
-                              const int32_t f[8]) {
+// first tested on those two fields alone; only the survivors — true record starts and the few positions whose
+// indices happen to be small — are checked in full.  Same PASS0 bitmap as k_check<MODE_EAGER, 1>.
+// Round 5: no workgroup barrier (round 2-4's k_eager staged 8 KiB tiles per 256-thread workgroup, and its waves
+// waited for one another at five barriers per tile and for one wave's survivor drain: 9.1 ms at 10 GB); every wave
+// streams its own tiles.  Lane l holds the 16-B pieces 1024 k + 16 l of the tile (k < 8; one coalesced 16-B load per piece) and
+// decides its 16 positions x = 1024 k + 16 l + j of each piece:
+//   * V(y) = "the int32 at y is in [-1, n_ref)" is evaluated once per byte offset y = x + 4 of the lane's positions
+//     (a 16-bit plane P_k per piece; refIdx at x + 4 — PosChecker.scala:43-63 / eager/Checker.scala:24-126);
+//   * nextRefIdx at x + 24 = y + 20 is the plane of lanes l + 1 and l + 2 (wave_shl1 DPP; lanes 62-63 take the next
+//     piece's lanes 0-1, and the tile's last piece the bytes past the tile, which lanes 0-3 load), so a position
+//     costs one V evaluation, not two;
+//   * the pieces also go to the wave's own LDS window (tile + 64 B), and the survivors S_k = P_k & (P_(l+1) >> 4 |
+//     P_(l+2) << 12) (0.5 % of positions: true records and a few others) to the wave's LDS bitmap of the tile and a
+//     wave-private queue; all 64 lanes check them in full from that window (a name or CIGAR ops that run past it
+//     from global memory) and clear the failing ones with LDS atomics;
+//   * the tile's 1 KiB of bitmap leaves as one coalesced 16-B store per lane.
+// Waves never wait for one another (each has its own LDS: 16 waves per CU), so the memory system sees 16 independent
+// streams per CU, and a survivor's dependent reads are LDS round trips, not memory ones.
+constexpr int kEwQ = 128;                // survivor queue per wave (a tile's survivors are queued in rounds)
+constexpr int kEwWaves = 4;
+constexpr int kEwHalo = 64;              // bytes past the tile in the window (>= 32: nextRefIdx of the last positions)
+constexpr int kEwWin = kTile + kEwHalo;  // per-wave LDS window
+// eager.Checker record-0 checks at position rel of a wave's window (win = the tile's bytes from base), given the
+// fixed fields f[]: check_first<true, true>'s pass/fail, straight from the bytes (no op-class / name-character
+// bitmaps: survivors are few, and a true record's name and CIGAR are short).
+SB_DEV bool eager_pass_win(const uint8_t *win, const StreamView &sv, int64_t x, int rel, const int32_t f[8]) {
   const int32_t bs = f[0], ri = f[1], rp = f[2], bmn = f[3], fnc = f[4], ls = f[5], nri = f[6], nrp = f[7];
   const int32_t lrn = bmn & 0xff;
   const uint32_t flag = ((uint32_t)fnc) >> 16;
   const int32_t nc = fnc & 0xffff;
-  const uint32_t rb0 = lensL ? ref_bits_lds(ri, rp, lensL, sv.nref) : ref_err(ri, rp, nullptr, sv.lens, sv.nref);
-  const uint32_t rb1 = lensL ? ref_bits_lds(nri, nrp, lensL, sv.nref) : ref_err(nri, nrp, nullptr, sv.lens, sv.nref);
-  if (rb0 | rb1 | (too_few_remaining(bs, lrn, nc, ls) ? 1u : 0u)) return false;
-  if (lrn < 2 || ((flag & 4u) == 0 && (ls == 0 || nc == 0))) return false;
-  if (win[rel + 35 + lrn] != 0) return false;  // name not NUL-terminated
-  // allowedReadNameChars, 4 name bytes per step (SWAR over an unaligned dword of the window)
-  const uint32_t *w32 = reinterpret_cast<const uint32_t *>(win);
-  for (int i = 0; i < lrn - 1; i += 4) {
-    const int a = rel + 36 + i;
-    const uint32_t w = __builtin_amdgcn_alignbyte(w32[(a >> 2) + 1], w32[a >> 2], (uint32_t)a & 3u);
-    const int left = lrn - 1 - i;
-    const uint32_t keep = left >= 4 ? 0x80808080u : (0x80808080u >> (8 * (4 - left)));
-    if (name_bad_bytes(w) & keep) return false;
-  }
+  if ((uint32_t)(lrn < 2) | (uint32_t)((flag & 4u) == 0 && (ls == 0 || nc == 0)) |
+      (uint32_t)too_few_remaining(bs, lrn, nc, ls))
+    return false;
+  if (ref_err(ri, rp, nullptr, sv.lens, sv.nref) | ref_err(nri, nrp, nullptr, sv.lens, sv.nref)) return false;
+  const gbytes u = gview(sv.u);
   const int c0 = rel + 36 + lrn;
-  const int in_win = min(nc, (kWin - c0) >> 2);  // ops inside the staged window, then HBM
+  if (c0 + 4 > kEwWin) {  // the name runs past the window (a position in the tile's last ~300 B): global memory
+    typedef const __attribute__((address_space(1))) uint32_t *g32;
+    if (u[x + 35 + lrn] != 0) return false;
+    for (int i = 0; i < lrn - 1; i += 4) {
+      const int64_t a = x + 36 + i;
+      const g32 q = (g32)(u + (a & ~(int64_t)3));
+      const uint32_t v = __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)a & 3u);
+      const int left = lrn - 1 - i;
+      const uint32_t keep = left >= 4 ? 0x80808080u : (0x80808080u >> (8 * (4 - left)));
+      if (name_bad_bytes(v) & keep) return false;
+    }
+  } else {
+    if (win[rel + 35 + lrn] != 0) return false;  // name not NUL-terminated
+    // allowedReadNameChars, 4 name bytes per step (SWAR over an unaligned dword of the window)
+    const uint32_t *w32 = reinterpret_cast<const uint32_t *>(win);
+    for (int i = 0; i < lrn - 1; i += 4) {
+      const int a = rel + 36 + i;
+      const uint32_t w = __builtin_amdgcn_alignbyte(w32[(a >> 2) + 1], w32[a >> 2], (uint32_t)a & 3u);
+      const int left = lrn - 1 - i;
+      const uint32_t keep = left >= 4 ? 0x80808080u : (0x80808080u >> (8 * (4 - left)));
+      if (name_bad_bytes(w) & keep) return false;
+    }
+  }
+  const int in_win = max(0, min(nc, (kEwWin - c0) >> 2));  // ops inside the window, then global memory
   for (int i = 0; i < in_win; i++)
     if ((win[c0 + 4 * i] & 0xfu) > 8u) return false;
-  const gbytes u = gview(sv.u);
   for (int i = in_win; i < nc; i++)
     if ((u[x + 36 + lrn + 4 * (int64_t)i] & 0xfu) > 8u) return false;
   return true;
 }
 
-__global__ __launch_bounds__(kCheckThreads) void k_eager(StreamView sv, int64_t x0, int R,
-                                                         unsigned long long *__restrict__ bitmap, int64_t tlo,
-                                                         int64_t thi) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_win[kWin + 64];
-  __shared__ int32_t s_lens[kEagerLens];
-  __shared__ uint16_t s_q[kEagerQ];
-  __shared__ uint32_t s_wn[kCheckThreads / 64];  // survivors per wave
-  __shared__ unsigned long long s_bits[kTile / 64];
+// lane l ← lane l + 1's v; lane 63 ← `last` (wave_shl1 DPP, the lane past the wave keeps the old value)
+SB_DEV uint32_t from_next_lane(uint32_t v, uint32_t last) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)last, (int)v, 0x130, 0xf, 0xf, false);
+}
+
+__global__ __launch_bounds__(64 * kEwWaves) void k_eager_wave(StreamView sv, int64_t x0, int R,
+                                                             unsigned long long *__restrict__ bitmap, int64_t tlo,
+                                                             int64_t thi) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_win[kEwWaves][kEwWin + 16];
+  __shared__ __attribute__((aligned(16))) uint32_t s_bm[kEwWaves][kTile / 32];
+  __shared__ uint16_t s_q[kEwWaves][kEwQ];
   const int lane = lane_id(), wv = (int)threadIdx.x >> 6;
-  const int32_t *lensL = nullptr;
-  if (sv.nref <= kEagerLens) {
-    for (int i = threadIdx.x; i < sv.nref; i += kCheckThreads) s_lens[i] = (int32_t)sv.lens[i];
-    lensL = s_lens;
-  }
-  const uint32_t nref1 = (uint32_t)sv.nref;  // idx + 1 <= n_ref  <=>  -1 <= idx < n_ref
+  uint8_t *win = s_win[wv];
+  const uint32_t *w32 = reinterpret_cast<const uint32_t *>(win);
+  uint32_t *bm = s_bm[wv];
+  uint16_t *q = s_q[wv];
+  const uint32_t nref1 = (uint32_t)sv.nref + 1u;  // -1 <= I < n_ref  <=>  (uint32)(I + 1) < n_ref + 1
   const int64_t x0a = x0 & ~(int64_t)63;
-  const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
-  uint16_t *q = s_q;
+  const gbytes u = gview(sv.u);
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   typedef const __attribute__((address_space(1))) u32x4 *g16;
-  // the window of the next tile is loaded into registers while this one is checked
-  constexpr int kPieces = (kWin / 16 + kCheckThreads - 1) / kCheckThreads;
-  u32x4 pre[kPieces];
-  auto fetch = [&](int64_t t) {
-    const g16 src = (g16)(gview(sv.u) + x0a + t * kTile);
-#pragma unroll
-    for (int k = 0; k < kPieces; k++) {
-      const int i = k * kCheckThreads + (int)threadIdx.x;
-      if (i < kWin / 16) pre[k] = src[i];
-    }
+  auto wave_sync = []() {  // order this wave's LDS accesses (no other wave touches its LDS)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
-  if (tlo + (int64_t)blockIdx.x < thi) fetch(tlo + blockIdx.x);
-  for (int64_t t = tlo + blockIdx.x; t < thi; t += gridDim.x) {
-    const int64_t base = x0a + t * kTile;
-    __syncthreads();
-    {
-      u32x4 *dst = reinterpret_cast<u32x4 *>(s_win);
+  const int64_t nt = thi - tlo;
+  for (int64_t ti = (int64_t)blockIdx.x * kEwWaves + wv; ti < nt; ti += (int64_t)gridDim.x * kEwWaves) {
+    const int64_t base = x0a + (tlo + ti) * kTile;
+    const g16 src = (g16)(u + base);
+    u32x4 pc[9];
 #pragma unroll
-      for (int k = 0; k < kPieces; k++) {
-        const int i = k * kCheckThreads + (int)threadIdx.x;
-        if (i < kWin / 16) dst[i] = pre[k];
+    for (int k = 0; k < 8; k++) pc[k] = src[64 * k + lane];
+    pc[8] = lane < kEwHalo / 16 ? src[512 + lane] : u32x4{0u, 0u, 0u, 0u};  // the bytes past the tile
+#pragma unroll
+    for (int k = 0; k < 8; k++) reinterpret_cast<u32x4 *>(win)[64 * k + lane] = pc[k];
+    if (lane < kEwHalo / 16) reinterpret_cast<u32x4 *>(win)[512 + lane] = pc[8];
+    // P[k] bit j = V(1024 k + 16 l + 4 + j)
+    uint32_t P[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+      const uint32_t n0 = from_next_lane(pc[k].x, k < 8 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)pc[k < 8 ? k + 1 : k].x) : 0u);
+      const uint32_t n1 = from_next_lane(pc[k].y, k < 8 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)pc[k < 8 ? k + 1 : k].y) : 0u);
+      const uint32_t wd[6] = {pc[k].x, pc[k].y, pc[k].z, pc[k].w, n0, n1};
+      uint32_t pl = 0;
+#pragma unroll
+      for (int j = 15; j >= 0; j--) {  // bit j appended last-first: pl = pl + pl + V
+        const int b = 4 + j;
+        const uint32_t I = (b & 3) ? __builtin_amdgcn_alignbyte(wd[(b >> 2) + 1], wd[b >> 2], b & 3) : wd[b >> 2];
+        pl = push_bit(pl, I + 1u < nref1);
       }
+      P[k] = pl;
     }
-    if (threadIdx.x < kTile / 64) s_bits[threadIdx.x] = 0ull;
-    __syncthreads();
-    if (t + gridDim.x < thi) fetch(t + gridDim.x);
-    // full eager check of the queued positions q[from, from + n), one per lane
-    auto drain = [&](int from, int n) {
-      if (lane < n) {
-        const int rel = q[from + lane];
+    // survivors: V(x + 4) && V(x + 24); x + 24 is bit j + 4 of lane l + 1's plane, or bit j - 12 of lane l + 2's
+    uint32_t S[8], cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t n1 = from_next_lane(P[k], (uint32_t)__builtin_amdgcn_readfirstlane((int)P[k + 1]));
+      const uint32_t n2 = from_next_lane(n1, (uint32_t)__builtin_amdgcn_readlane((int)P[k + 1], 1));
+      S[k] = P[k] & ((n1 >> 4) | (n2 << 12)) & 0xffffu;
+      cnt += (uint32_t)__popc(S[k]);
+      reinterpret_cast<uint16_t *>(bm)[64 * k + lane] = (uint16_t)S[k];
+    }
+    const uint32_t incl = wave_incl_scan_u32(cnt), total = (uint32_t)__shfl((int)incl, 63, 64);
+    for (uint32_t r0 = 0; r0 < total; r0 += kEwQ) {  // (one round unless the tile has > kEwQ survivors)
+      uint32_t at = incl - cnt;
+      if (at < r0 + kEwQ && at + cnt > r0) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          for (uint32_t m = S[k]; m; m &= m - 1, at++)
+            if (at >= r0 && at < r0 + kEwQ) q[at - r0] = (uint16_t)(1024 * k + 16 * lane + __builtin_ctz(m));
+        }
+      }
+      wave_sync();
+      const uint32_t nq = min((uint32_t)kEwQ, total - r0);
+      for (uint32_t i = (uint32_t)lane; i < nq; i += 64) {
+        const int rel = q[i];
         const int o = rel & 3, d = rel >> 2;
         int32_t f[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) f[k] = (int32_t)__builtin_amdgcn_alignbyte(w32[d + k + 1], w32[d + k], o);
-        if (eager_pass_direct(s_win, sv, lensL, base + rel, rel, f)) atomicOr(&s_bits[rel >> 6], 1ull << (rel & 63));
+        if (!eager_pass_win(win, sv, base + rel, rel, f)) atomicAnd(&bm[rel >> 5], ~(1u << (rel & 31)));
       }
-    };
-    // prefilter: bit 31 - (4j + o) of sm = position 4 (j·kCheckThreads + thread) + o survives
-    uint32_t sm = 0;
-#pragma unroll
-    for (int j = 0; j < kTile / (4 * kCheckThreads); j++) {
-      const int g = j * kCheckThreads + threadIdx.x;  // group of 4 consecutive positions
-      const uint32_t a1 = w32[g + 1], a2 = w32[g + 2], a6 = w32[g + 6], a7 = w32[g + 7];
-#pragma unroll
-      for (int o = 0; o < 4; o++) {
-        const uint32_t ri = __builtin_amdgcn_alignbyte(a2, a1, o), nri = __builtin_amdgcn_alignbyte(a7, a6, o);
-        sm = push_bit(sm, ri + 1u <= nref1 && nri + 1u <= nref1);  // position (j, o) at bit 31 - (4 j + o)
-      }
+      wave_sync();
     }
-    // the workgroup's survivors go to one queue (kEagerQ at a time), drained 64 at a time by the waves in turn: a
-    // tile has ~40 (0.5 % of positions), so one wave usually checks them all in one full-width round instead of
-    // every wave running a mostly idle one
-    const uint32_t n = (uint32_t)__popc(sm);
-    const uint32_t incl = wave_incl_scan_u32(n);
-    if (lane == 63) s_wn[wv] = incl;
-    __syncthreads();
-    uint32_t wbase = 0, total = 0;
-#pragma unroll
-    for (int k = 0; k < kCheckThreads / 64; k++) {
-      const uint32_t c = s_wn[k];
-      wbase += k < wv ? c : 0u;
-      total += c;
-    }
-    for (uint32_t r0 = 0; r0 < total; r0 += kEagerQ) {
-      uint32_t at = wbase + incl - n;
-      for (uint32_t m = sm; m && at < r0 + kEagerQ; m &= m - 1, at++) {
-        if (at >= r0) {
-          const int bit = 31 - __builtin_ctz(m);
-          q[at - r0] = (uint16_t)(4 * ((bit >> 2) * kCheckThreads + (int)threadIdx.x) + (bit & 3));
-        }
-      }
-      __syncthreads();
-      const int nq = (int)min((uint32_t)kEagerQ, total - r0);
-      for (int from = 64 * wv; from < nq; from += kCheckThreads) drain(from, min(64, nq - from));
-      __syncthreads();
-    }
-    __syncthreads();
-    if (threadIdx.x < kTile / 64) bitmap[((base - x0a) >> 6) + threadIdx.x] = s_bits[threadIdx.x];
+    const u32x4 out = reinterpret_cast<const u32x4 *>(bm)[lane];
+    reinterpret_cast<u32x4 *>(bitmap + ((base - x0a) >> 6))[lane] = out;
+    wave_sync();  // (the next tile's LDS writes come after every lane's reads)
   }
 }
 
@@ -1759,9 +1778,10 @@ hipError_t launch_check_eager_pass0(StreamView sv, int64_t x0, int64_t x1, int32
   int64_t tlo, thi;
   interior_tiles(sv, x0, x1, &tlo, &thi);
   const int64_t nt = ntiles_of(x0, x1), ni = thi - tlo;
-  if (ni > 0)
-    hipLaunchKernelGGL(k_eager, dim3(resident_grid<MODE_EAGER, 1>(ni)), dim3(kCheckThreads), 0, s, sv, x0, (int)R,
-                       bitmap, tlo, thi);
+  if (ni > 0) {  // ~10 tiles per wave: a wave that finishes early takes the next workgroup
+    const int64_t g = std::max<int64_t>(1, std::min<int64_t>((ni + 10 * kEwWaves - 1) / (10 * kEwWaves), 131072));
+    hipLaunchKernelGGL(k_eager_wave, dim3((unsigned)g), dim3(64 * kEwWaves), 0, s, sv, x0, (int)R, bitmap, tlo, thi);
+  }
   if (nt > ni)
     hipLaunchKernelGGL((k_check<MODE_EAGER, 2>), dim3(check_grid(nt - ni)), dim3(kCheckThreads), 0, s, sv, x0, x1, R,
                        CountsDev{}, bitmap, nullptr, tlo, thi);

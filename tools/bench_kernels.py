@@ -62,6 +62,11 @@ def main():
         timed("check_bykey", lambda: f.check_full_counts(0, U, by_key=True), "check_full")
     if "check_eager" in only:
         timed("check_eager", lambda: f.check_eager(0, U), "check_eager")
+        p0 = []
+        for _ in range(args.reps):  # the record-0 pass alone (k_eager_wave + boundary tiles), bitmap left on the device
+            f.check_eager_device(0, U)
+            p0.append(f.kernel_ms("check_eager_pass0"))
+        ms["check_eager_pass0"] = round(float(np.median(p0)), 3)
     if "splits" in only:
         f.check_full_counts(0, U)
         t0 = time.perf_counter()
@@ -73,7 +78,7 @@ def main():
     gbs = {}
     if "inflate" in ms:
         gbs["inflate"] = round((C + U) / ms["inflate"] / 1e6, 2)
-    for k in ("check_full", "check_bykey", "check_eager"):
+    for k in ("check_full", "check_bykey", "check_eager", "check_eager_pass0"):
         if k in ms:
             gbs[k] = round((U + U / 8) / ms[k] / 1e6, 2)
     out.update({"ms": ms, "alg_GBps": gbs})
