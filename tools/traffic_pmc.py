@@ -27,7 +27,7 @@ KERNELS = {"k_check_bits": "sbam::k_check_bits", "k_check<0, 0>": "sbam::k_check
            "k_scan_count": "sbam::k_scan_count", "k_scan_write": "sbam::k_scan_write", "k_scan_slots": "sbam::k_scan_slots",
            "k_scan_slots_wide": "sbam::k_scan_slots_wide<32>",
            "k_scan_compact": "sbam::k_scan_compact",
-           "k_record_counts": "sbam::k_record_counts", "k_eager": "sbam::k_eager"}
+           "k_record_counts": "sbam::k_record_counts", "k_eager_wave": "sbam::k_eager_wave"}
 
 
 def per_dispatch(d, counter, scale=1024.0):
