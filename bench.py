@@ -183,6 +183,9 @@ def main():
                          "(two contexts: window w+1's host staging and PCIe copy overlap window w's kernels; "
                          "both inside the timed step)")
     ap.add_argument("--read-len", type=int, default=150, help="0 = long-read config (configs[4])")
+    ap.add_argument("--contigs", type=int, default=0,
+                    help="check against N contig lengths (the file's 84, then N - 84 more: a scaffold-level reference, "
+                         "so refIdx values up to N - 1 are in range); 0 = the file's own")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (RCCL, the product path); gloo only to rehearse N ranks on one GPU (--device)")
     ap.add_argument("--device", type=int, default=None, help="GPU index (default LOCAL_RANK)")
@@ -222,6 +225,9 @@ def main():
                                 threads=threads, read_len=args.read_len, distinct=args.tiles > 1,
                                 cycle=max(args.tiles, 1))
     setup_s = time.time() - t
+    if args.contigs > len(s.contig_lengths):  # many-contig reference: lengths past the 84 real ones
+        extra = np.random.default_rng(args.seed).integers(1000, 1 << 28, args.contigs - len(s.contig_lengths))
+        s.contig_lengths = np.concatenate([np.asarray(s.contig_lengths, np.int64), extra.astype(np.int64)])
     plans = sdist.plan_shards(s.size, split_size, world)  # rank-level plans (what all_gather sees)
     plan = plans[rank]
     W = args.windows
@@ -469,7 +475,8 @@ def main():
                        "file_gb": round(s.size / 1e9, 3), "uncompressed_gb_per_gpu": round(U / 1e9, 3),
                        "records": s.n_records, "blocks_per_gpu": nblocks, "split_mb": args.split_mb,
                        "windows_per_gpu": W, "parallelism": f"shard{world}",
-                       "tiles": min(args.tiles, s.copies), "setup_s": round(setup_s, 1)},
+                       "tiles": min(args.tiles, s.copies), "setup_s": round(setup_s, 1),
+                       **({"contigs": len(s.contig_lengths)} if args.contigs else {})},
             "uncompressed_gbps": round(U * world * args.steps / elapsed / 1e9, 3),
             "kernel_ms": {k: round(v, 3) for k, v in avg.items()},
             "roofline": {"bound": "hbm", "kernel": names[dom], "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,

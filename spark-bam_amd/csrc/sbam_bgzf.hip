@@ -27,12 +27,7 @@ SB_DEV uint32_t brev(uint32_t code, int len) { return __builtin_bitreverse32(cod
 // 1. BGZF header scan
 // ================================================================================================
 constexpr int kScanThreads = 256;
-#ifndef SBAM_SCAN_PREFETCH  // k_scan_slots loads iteration i + 1 while ranking iteration i's candidates
-#define SBAM_SCAN_PREFETCH 1
-#endif
-#ifndef SBAM_SCAN_WIDE  // k_scan_slots_wide<SBAM_SCAN_WIDE> (positions per thread and iteration) instead of
-#define SBAM_SCAN_WIDE 32  // k_scan_slots (0); scan at 10 GB: 16 / 32 / 64 -> 2.51 / 2.14 / 2.20 ms, k_scan_slots 2.83
-#endif
+constexpr int kScanWide = 32;  // positions per thread and iteration of k_scan_slots_wide
 constexpr int kScanStep = kScanThreads * 16;  // bytes per workgroup iteration
 
 // 16 candidate bits for positions q0..q0+15 given the 32 bytes at q0 (w[0..7] little-endian words).
@@ -169,82 +164,14 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_write(const uint8_t *__re
   }
 }
 
-// One-pass form (round 3): the same candidates written to chunk b's kScanSlots fixed slots, its count to
-// chunk_counts[b] (slots past kScanSlots are not written; *overflow is set and the caller runs k_scan_write with
-// the exact offsets instead), then k_scan_compact moves the slots into file order.  Reads the compressed bytes
-// once instead of twice (k_scan_count + k_scan_write).
-__global__ __launch_bounds__(kScanThreads) void k_scan_slots(const uint8_t *__restrict__ d, int64_t D,
-                                                              int32_t *__restrict__ chunk_counts,
-                                                              Candidate *__restrict__ slots,
-                                                              unsigned long long *__restrict__ overflow) {
-  const int64_t cbase = (int64_t)blockIdx.x * kScanChunk;
-  const int64_t cend = min(cbase + (int64_t)kScanChunk, D);
-  __shared__ int s_any;
-  __shared__ int s_wsum[kScanThreads / 64];
-  Candidate *out = slots + (int64_t)blockIdx.x * kScanSlots;
-  int run = 0;
-#if SBAM_SCAN_PREFETCH
-  // the next iteration's 32 B are loaded before this one's candidates are ranked (two barriers), so a workgroup
-  // keeps 8 KiB in flight instead of 4
-  uint32_t wn[8];
-  if (cbase + threadIdx.x * 16 < cend) load32(d, cbase + threadIdx.x * 16, wn);
-#endif
-  for (int64_t it = cbase; it < cend; it += kScanStep) {
-    const int64_t q0 = it + threadIdx.x * 16;
-    uint32_t bits = 0;
-#if SBAM_SCAN_PREFETCH
-    uint32_t w[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) w[k] = wn[k];
-    if (q0 + kScanStep < cend) load32(d, q0 + kScanStep, wn);
-    if (q0 < cend) {
-      bits = header_bits16(w, q0, D);
-      if (q0 + 16 > cend) bits &= (1u << (cend - q0)) - 1u;
-    }
-#else
-    if (q0 < cend) {
-      uint32_t w[8];
-      load32(d, q0, w);
-      bits = header_bits16(w, q0, D);
-      if (q0 + 16 > cend) bits &= (1u << (cend - q0)) - 1u;
-    }
-#endif
-    if (threadIdx.x == 0) s_any = 0;
-    __syncthreads();
-    if (bits) s_any = 1;
-    __syncthreads();
-    if (s_any) {  // rare: ordered rank = wave prefix + preceding waves
-      const int c = __popc(bits);
-      int incl = c;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(incl, o, 64);
-        if (lane_id() >= o) incl += t;
-      }
-      if (lane_id() == 63) s_wsum[threadIdx.x >> 6] = incl;
-      __syncthreads();
-      int before = incl - c;
-      for (int wv = 0; wv < (int)(threadIdx.x >> 6); wv++) before += s_wsum[wv];
-      int slot = run + before;
-      while (bits) {
-        const int i = __ffs(bits) - 1;
-        bits &= bits - 1;
-        if (slot < kScanSlots) fill_candidate(d, D, q0 + i, out[slot]);
-        slot++;
-      }
-      run += s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    chunk_counts[blockIdx.x] = run;
-    if (run > kScanSlots) atomicOr(overflow, 1ull);
-  }
-}
-
-// Wide form of k_scan_slots: P positions per thread and iteration (P + 16 B loaded as 16-B pieces, the next one's
-// prefetched while this one's candidates are ranked), and one barrier per iteration without candidates (an
-// "any candidate" flag in three rotating LDS words: the one for iteration i + 1 is cleared before iteration i's
-// barrier, after every read of it in iteration i - 2).  Same slots, counts and overflow as k_scan_slots.
+// One-pass form (round 3): the candidates of chunk b written to its kScanSlots fixed slots, its count to
+// chunk_counts[b] (slots past kScanSlots are not written; *overflow is set and the caller runs k_scan_write with the
+// exact offsets instead), then k_scan_compact moves the slots into file order — the compressed bytes are read once
+// instead of twice (k_scan_count + k_scan_write).  Round 4: P positions per thread and iteration (P + 16 B loaded as
+// 16-B pieces, the next one's prefetched while this one's candidates are ranked), and one barrier per iteration
+// without candidates (an "any candidate" flag in three rotating LDS words: the one for iteration i + 1 is cleared
+// before iteration i's barrier, after every read of it in iteration i - 2).  Scan at 10 GB with P = 16 / 32 / 64:
+// 2.51 / 2.14 / 2.20 ms; 16 positions with three barriers per iteration (round 3): 2.83.
 template <int P>
 SB_DEV void load_wide(const uint8_t *d, int64_t q0, uint32_t w[P / 4 + 4]) {
 #pragma unroll
@@ -426,13 +353,8 @@ hipError_t launch_scan_slots(const uint8_t *d, int64_t D, int32_t *cc, int64_t n
                              int64_t *overflow, hipStream_t s) {
   (void)hipMemsetAsync(overflow, 0, sizeof(int64_t), s);
   if (nchunks == 0) return hipSuccess;
-#if SBAM_SCAN_WIDE
-  hipLaunchKernelGGL(k_scan_slots_wide<SBAM_SCAN_WIDE>, dim3((unsigned)nchunks), dim3(kScanThreads), 0, s, d, D, cc,
+  hipLaunchKernelGGL(k_scan_slots_wide<kScanWide>, dim3((unsigned)nchunks), dim3(kScanThreads), 0, s, d, D, cc,
                      slots, reinterpret_cast<unsigned long long *>(overflow));
-#else
-  hipLaunchKernelGGL(k_scan_slots, dim3((unsigned)nchunks), dim3(kScanThreads), 0, s, d, D, cc, slots,
-                     reinterpret_cast<unsigned long long *>(overflow));
-#endif
   return hipGetLastError();
 }
 hipError_t launch_scan_compact(const Candidate *slots, const int32_t *cc, const int64_t *off, int64_t nchunks,

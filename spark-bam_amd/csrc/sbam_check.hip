@@ -23,21 +23,6 @@
 
 #include "sbam_internal.h"
 
-// k_check workgroups per CU the register budget is sized for (launch bounds): boundary tiles / interior tiles
-#ifndef SBAM_CHECK_WGS
-#define SBAM_CHECK_WGS 4
-#endif
-#ifndef SBAM_CHECK_WGS_INT
-#define SBAM_CHECK_WGS_INT 5
-#endif
-#ifndef SBAM_CHECK_WGS_BITS
-#define SBAM_CHECK_WGS_BITS 5  // k_check_bits (6 spills a few constants: +7 GB scratch traffic, same time; round 4 with
-                               // the LDS trimmed to 26.8 KB so that 6 workgroups fit: 41.5 vs 41.2 ms — not latency-bound)
-#endif
-#ifndef SBAM_LDS_LENS
-#define SBAM_LDS_LENS 4096
-#endif
-
 namespace sbam {
 
 #define SB_DEV __device__ __forceinline__
@@ -51,7 +36,11 @@ constexpr int kHalo = 768;                  // staged bytes past the tile (fixed
 constexpr int kWin = kTile + kHalo;         // staged window (multiple of 16)
 constexpr int kOpcWords = kWin / 128 + 4;   // per residue class: one bit per 4 window bytes (+ pad)
 constexpr int kNameWords = kWin / 32 + 4;   // one bit per window byte (+ pad)
-constexpr int kLdsLens = SBAM_LDS_LENS;     // contig lengths kept in LDS when n_ref fits
+constexpr int kLdsLens = 4096;              // contig lengths kept in LDS when n_ref fits
+// workgroups per CU the register budget is sized for (launch bounds): k_check over boundary tiles / interior tiles,
+// k_check_bits (6: a few constants spill, +7 GB scratch traffic, same time; round 4 with the LDS trimmed to 26.8 KB
+// so that 6 workgroups fit: 41.5 vs 41.2 ms — not latency-bound)
+constexpr int kCheckWgs = 4, kCheckWgsInt = 5, kCheckWgsBits = 5;
 constexpr int kFlushTiles = 7;              // 7 tiles x 32 positions per lane < 255 (8-bit planes / counters)
 static_assert(kWin % 16 == 0, "window");
 static_assert((kTile / (4 * kCheckThreads)) % 2 == 0, "groups pair up within a tile (add4_paired)");
@@ -935,7 +924,7 @@ SB_DEV void bykey_count(uint32_t *s_cnt, int lane, bool counted, uint32_t key, u
 // PART 0: every tile of [x0, x1); PART 1: only the interior tiles [tlo, thi) (interior_tiles), compiled without
 // the boundary path so its register budget is its own; PART 2: every tile except [tlo, thi).
 template <int MODE, int PART>
-__global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBAM_CHECK_WGS) void k_check(
+__global__ __launch_bounds__(kCheckThreads, PART == 1 ? kCheckWgsInt : kCheckWgs) void k_check(
     StreamView sv, int64_t x0, int64_t x1, int R, CountsDev cd, unsigned long long *__restrict__ bitmap,
     uint32_t *__restrict__ words, int64_t tlo, int64_t thi) {
   constexpr bool EAGER = MODE == MODE_EAGER;
@@ -1113,7 +1102,8 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? SBAM_CHECK_WGS_INT : SBA
 //     position), decoded per key with one 3-input op and counted by v_bcnt; PASS0 is the NOR of the planes,
 //     transposed across 8 lanes (ds_swizzle) into bitmap dwords.
 // A position with a long name or op array (past the 64 bytes / ops one bitmap read covers) is redone by check_first
-// and patched into the planes.  Interior tiles only (no EOF in reach), R > 0, n_ref <= kLdsLens (lengths in LDS).
+// and patched into the planes.  Interior tiles only (no EOF in reach), R > 0; the contig lengths are in LDS when
+// n_ref <= kLdsLens, else in the device table (round 5: many-contig references took the general k_check before).
 SB_DEV uint32_t push_bit(uint32_t p, bool c) {  // (the carry-out goes to VCC: a dead SGPR-pair output made the
   uint32_t r;                                    // compiler reuse one pair and pad with s_nop between VALU writes)
   asm("v_addc_co_u32 %0, vcc, %1, %1, %2" : "=v"(r) : "v"(p), "s"(__ballot(c)) : "vcc");
@@ -1139,7 +1129,7 @@ SB_DEV uint32_t ctz64(uint32_t lo, uint32_t hi) { return min(ffbl(lo), ffbl(hi) 
 // plane i of X[] holds flag kBitFlag[i] (the flags an interior position can fail)
 constexpr int kBitFlag[16] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 13, 15, 16, 17, 18};
 
-__global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bits(StreamView sv, int64_t x0, int R,
+__global__ __launch_bounds__(kCheckThreads, kCheckWgsBits) void k_check_bits(StreamView sv, int64_t x0, int R,
                                                                                    CountsDev cd,
                                                                                    unsigned long long *__restrict__ bitmap,
                                                                                    int64_t tlo, int64_t thi) {
@@ -1159,7 +1149,11 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bi
   for (int i = t; i < 19 * 19; i += kCheckThreads) s_pair[i] = 0;
   for (int i = t; i < 19 + 21; i += kCheckThreads) s_acc[i] = 0;
   const int32_t nref = sv.nref;
-  for (int i = t; i <= nref; i += kCheckThreads) s_lens[i] = i < nref ? (int32_t)sv.lens[i] : 0x7fffffff;
+  // contig lengths in LDS when they fit (the dynamic allocation is n_ref + 1 entries then); else the rare probes
+  // below read the device table (L2-resident, ~1 % of offsets)
+  const bool lds_lens = nref <= kLdsLens;
+  if (lds_lens)
+    for (int i = t; i <= nref; i += kCheckThreads) s_lens[i] = i < nref ? (int32_t)sv.lens[i] : 0x7fffffff;
   const int64_t x0a = x0 & ~(int64_t)63;
   const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
   // per-lane counters, two 16-bit halves per register: c < 16 = plane c's flag total, 16 + k - 1 = key k
@@ -1214,7 +1208,8 @@ __global__ __launch_bounds__(kCheckThreads, SBAM_CHECK_WGS_BITS) void k_check_bi
           const int y = 4 * (((k >> 2) + r0) * kCheckThreads + t) + (k & 3);
           const int32_t I = (int32_t)__builtin_amdgcn_alignbyte(w32[(y >> 2) + 1], w32[y >> 2], y & 3);
           const int32_t I4 = (int32_t)__builtin_amdgcn_alignbyte(w32[(y >> 2) + 2], w32[(y >> 2) + 1], y & 3);
-          pc |= (I >= 0 && I4 > s_lens[I >= 0 ? I : 0]) ? (1u << b) : 0u;
+          const int64_t len = lds_lens ? (int64_t)s_lens[I >= 0 ? I : 0] : sv.lens[I >= 0 ? I : 0];
+          pc |= (I >= 0 && (int64_t)I4 > len) ? (1u << b) : 0u;
         }
         return pc;
       };
@@ -1708,7 +1703,7 @@ hipError_t launch_check_full_counts(StreamView sv, int64_t x0, int64_t x1, int32
   if (by_key) {
     hipLaunchKernelGGL((k_check<MODE_BYKEY, 0>), dim3(check_grid(ntiles_of(x0, x1))), dim3(kCheckThreads), 0, s, sv,
                        x0, x1, R, cd, bitmap, nullptr, (int64_t)0, (int64_t)0);
-  } else if (R > 0 && sv.nref <= kLdsLens) {
+  } else if (R > 0) {
     // interior tiles bit-sliced (k_check_bits), the boundary tiles by k_check<MODE_COUNTS, 2>; between them every
     // tile's PASS0 count when cd.tile_pass0 is set
     *tiles_counted = cd.tile_pass0 != nullptr;
@@ -1716,7 +1711,7 @@ hipError_t launch_check_full_counts(StreamView sv, int64_t x0, int64_t x1, int32
     interior_tiles(sv, x0, x1, &tlo, &thi);
     const int64_t nt = ntiles_of(x0, x1), ni = thi - tlo;
     if (ni > 0) {
-      const size_t shmem = ((size_t)sv.nref + 1) * sizeof(int32_t);
+      const size_t shmem = (sv.nref <= kLdsLens ? (size_t)sv.nref + 1 : 1) * sizeof(int32_t);
       hipLaunchKernelGGL(k_check_bits, dim3(bits_grid(ni, shmem)), dim3(kCheckThreads), shmem, s, sv, x0, R, cd,
                          bitmap, tlo, thi);
     }

@@ -734,10 +734,7 @@ namespace wd {
 // in distinct banks (at 512 = 16 dwords, lanes k and k + 2 shared a bank: 20.9 G conflict cycles per launch at
 // 10 GB, 7.0 G at 544; decode 67.0 → 63.8 ms).  An XOR-swizzled root-table index changed nothing (62.3 vs 62.6 G
 // over three launches): the conflicts were the window reads'.
-#ifndef SBAM_KK
-#define SBAM_KK 544
-#endif
-constexpr int kK = SBAM_KK;                // bits per lane segment
+constexpr int kK = 544;                    // bits per lane segment
 constexpr int kWinDw = 64 * kK / 32 + 16;  // staged input dwords per round (start alignment + lookahead)
 // 9-bit roots for both alphabets (zlib's ENOUGH bounds: 852 literal/length and 592 distance entries with
 // sub-tables), interleaved: the root entry of 9-bit prefix b in state st (0: literal/length, 1: distance after a
@@ -749,46 +746,24 @@ constexpr int kLitRoot = 9, kDistRoot = 9;
 constexpr int kLitSub = 340, kDistSub = 80;  // ENOUGH - root: 852 - 512 and 592 - 512 at root 9
 constexpr int kLitSubOff = 2 << kLitRoot, kDistSubOff = kLitSubOff + kLitSub;
 constexpr int kTab = kDistSubOff + kDistSub;
-#ifndef SBAM_RWIN
-#define SBAM_RWIN 1
-#endif
-#ifndef SBAM_CP  // (8 × 12 and 16 × 6 symbols: within 0.2 ms of 12 × 8)
-#define SBAM_CP 12
-#endif
-constexpr int kCp = SBAM_CP;                // checkpoints per lane
-constexpr int kCpSteps = 96 / SBAM_CP;      // symbols between checkpoints
+constexpr int kCp = 12;                     // checkpoints per lane (8 × 12 and 16 × 6 symbols: within 0.2 ms of 12 × 8)
+constexpr int kCpSteps = 96 / kCp;          // symbols between checkpoints
 // Lanes > 0 start decoding kWarm bits before their segment, so that by the segment start their path has usually
 // resynchronised with the true one: the first symbol boundary at or after the segment start ("entry") then equals
 // the left neighbour's exit and phase A's counts from the entry on need no phase-B re-decode.  Decode at 10 GB:
 // no warm-up 79.5 ms; 128 bits 74.8; 256: 71.6; 384: 69.6; 512 (one segment; lane 1 from the round's true start):
 // 68.5; 640: 70.1; 1024: 76.7.  Round 3 (544-bit segments, register tokens, re-decode only to the rejoin point):
 // 192: 70.5; 288: 65.7; 384: 59.9; 544: 51.1; 640: 49.6; 768: 49.8; 960: 52.2.
-#ifndef SBAM_WARM
-#define SBAM_WARM 640
-#endif
-constexpr int kWarm = SBAM_WARM;
+constexpr int kWarm = 640;
 // Phase A keeps the tokens of its first kTR symbol steps in registers (two per VGPR, step j in half j & 1 of
 // tr[j / 2]: the steps are unrolled, so every index is static).  A lane whose phase-A path is the true one (the
 // common case after the warm-up) then only stores them in phase C; it decodes again only past step kTR.  With the
 // round-3 v2 step (38 VALU instead of 58) the register budget is what limits kTR: 96 tokens spilled 48 VGPRs to
 // scratch, 80 spill 11 (decode at 10 GB: 96 → 47.7 ms, 80 → 45.9; 72: 47.5, its phase C re-decodes more tails).
-#ifndef SBAM_CDUMP  // register tokens stored through LDS as whole 16-B chunks (1) or per lane (0)
-#define SBAM_CDUMP 0
-#endif
-#ifndef SBAM_WPRE  // next-window prefetch into registers (WinPre): 1 during phase C, 2 during the table build
-#define SBAM_WPRE 0
-#endif
-#ifndef SBAM_TR
-#define SBAM_TR 80
-#endif
-constexpr int kTR = SBAM_TR;
-#ifndef SBAM_STAGE_UNROLL  // window staging: LDS DMA (2), all loads into VGPRs before one wait (1), a load-wait-store
-                           // loop (0); decode at 10 GB 41.07 / 41.46 / 41.93 ms
-#define SBAM_STAGE_UNROLL 2
-#endif
-#ifndef SBAM_TR_PIN  // register tokens forced into VGPRs before phase C's stores: 1 before the re-decode, 2 after it
-#define SBAM_TR_PIN 2
-#endif
+// (Round 4, measured and dropped, DESIGN.md §Inflate: the register tokens stored through LDS as whole 16-B chunks,
+// 55.0 ms; the next window prefetched into registers during phase C or the table build, 44.3 ms; the register tokens
+// pinned before phase C's re-decode instead of after it.)
+constexpr int kTR = 80;
 static_assert(kTR % 2 == 0 && kTR <= kCp * kCpSteps, "register tokens come from the unrolled checkpoint steps");
 static_assert(kTR % kCpSteps == 0, "the state after step kTR (stR) is saved at a checkpoint");
 constexpr int kScratchDw = 256;    // window tail that doubles as header / table-build scratch
@@ -1027,7 +1002,6 @@ SB_DEV void wave_stage(uint32_t *win, const uint32_t *base, int64_t base_dw, int
   constexpr int kN = (wd::kWinDw + 255) / 256;
   const int lane = (int)threadIdx.x;
   __syncthreads();  // every lane is done with the previous window
-#if SBAM_STAGE_UNROLL == 2
   // LDS DMA (global_load_lds_dwordx4: lane l's 16 B land at the LDS base + 16 l), no VGPRs; lanes past the buffer
   // load its last 16 B instead of zeros (bits past the payload only ever end a speculative path: ST_OUT)
   {
@@ -1043,66 +1017,8 @@ SB_DEV void wave_stage(uint32_t *win, const uint32_t *base, int64_t base_dw, int
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-#elif SBAM_STAGE_UNROLL
-  uint4 v[kN];
-#pragma unroll
-  for (int k = 0; k < kN; k++) {
-    const int i = lane * 4 + 256 * k;
-    const int64_t g = base_dw + wq_dw + i;
-    v[k] = (i < wd::kWinDw && g + 4 <= lim_dw) ? *reinterpret_cast<const uint4 *>(base + wq_dw + i)
-                                                 : make_uint4(0, 0, 0, 0);
-  }
-#pragma unroll
-  for (int k = 0; k < kN; k++) {
-    const int i = lane * 4 + 256 * k;
-    if (i < wd::kWinDw) *reinterpret_cast<uint4 *>(win + i) = v[k];
-  }
-#else
-  for (int i = lane * 4; i < wd::kWinDw; i += 256) {
-    const int64_t g = base_dw + wq_dw + i;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (g + 4 <= lim_dw) v = *reinterpret_cast<const uint4 *>(base + wq_dw + i);
-    *reinterpret_cast<uint4 *>(win + i) = v;
-  }
-#endif
   __syncthreads();
 }
-// The same window loaded into registers ahead of time (WinPre::fetch as soon as the next window's start is known:
-// after phase B for the next round or block header, after the header for the first round), stored into LDS when
-// the window is free (WinPre::stage): the loads' latency hides behind phase C or the table build.
-struct WinPre {
-  static constexpr int kN = (wd::kWinDw + 255) / 256;
-  uint4 v[kN];
-  int wq = -1;  // window start (dwords) of v, or -1
-  SB_DEV void fetch(const uint32_t *base, int64_t base_dw, int wq_dw, int64_t lim_dw) {
-    const int lane = (int)threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < kN; k++) {
-      const int i = lane * 4 + 256 * k;
-      const int64_t g = base_dw + wq_dw + i;
-      v[k] = (i < wd::kWinDw && g + 4 <= lim_dw) ? *reinterpret_cast<const uint4 *>(base + wq_dw + i)
-                                                   : make_uint4(0, 0, 0, 0);
-    }
-    wq = wq_dw;
-  }
-  // stage window wq_dw: from the registers when they hold it, else loaded now
-  SB_DEV void stage(uint32_t *win, const uint32_t *base, int64_t base_dw, int wq_dw, int64_t lim_dw) {
-    if (SBAM_WPRE && wq == wq_dw) {
-      const int lane = (int)threadIdx.x;
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < kN; k++) {
-        const int i = lane * 4 + 256 * k;
-        if (i < wd::kWinDw) *reinterpret_cast<uint4 *>(win + i) = v[k];
-      }
-      __syncthreads();
-    } else {
-      wave_stage(win, base, base_dw, wq_dw, lim_dw);
-    }
-    wq = -1;
-  }
-};
-
 // Result of one lane's decode of its segment from a given start: counts, exit key (pos << 10 | state << 9 |
 // pending length) and stop.
 struct SegResult {
@@ -1170,11 +1086,10 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
   const uint64_t wt0_ = wt_;
 #endif
 
-  WinPre pre;
   for (bool fin = false; ok && !fin;) {
     // ---- block header
     int wq = (pos >> 7) << 7;
-    pre.stage(L.win, base, base_dw, wq >> 5, lim_dw);
+    wave_stage(L.win, base, base_dw, wq >> 5, lim_dw);
     WMARK(12);
     if (pos + 3 > pend) { ok = false; break; }
     HBits h;
@@ -1324,7 +1239,6 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
     if (h.pos > pend) { ok = false; break; }
     WMARK(0);
     WADD(9, 1);
-    if (SBAM_WPRE & 2) pre.fetch(base, base_dw, (h.pos >> 7) << 2, lim_dw);  // the first round's window, during the build
     if (!wave_build<true>(L, 288, hdist, kDistSubOff, kDistSub)) { ok = false; break; }
     if (!wave_build<false>(L, 0, hlit, kLitSubOff, kLitSub)) { ok = false; break; }
     WMARK(1);
@@ -1334,7 +1248,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
     for (;;) {
       const int Sp = (int)(S >> 10);
       wq = (Sp >> 7) << 7;
-      pre.stage(L.win, base, base_dw, wq >> 5, lim_dw);
+      wave_stage(L.win, base, base_dw, wq >> 5, lim_dw);
       const uint32_t *wp = L.win - (wq >> 5);  // wp[pos >> 5]: the staged dword holding bit pos
       WMARK(2);
       WADD(6, 1);
@@ -1377,7 +1291,6 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         }
         WMARK(13);
         entry = ((uint32_t)rp << 10) | (st4 << 7) | pl;
-#if SBAM_RWIN
         // the window dwords W, W + 1, W + 2 of the reader (W = rp >> 5) in registers: a symbol is at most 28 bits,
         // so the next reader is in W or W + 1, and dword W + 2 of the new reader is loaded a whole step before use
         // (one LDS round trip less on a step's dependent chain: root entry, sub-table entry; decode 46.0 → 45.7 ms.
@@ -1389,7 +1302,6 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
           wB = q[1];
           wC = q[2];
         }
-#endif
         // one symbol, predicated: a lane that is done (stopped out of the data, or past its segment) decodes the
         // same symbol again and commits nothing, so the steps need no exec-mask branches
         // ST: the step's index when it is below kTR (its token goes to tr), else -1
@@ -1399,11 +1311,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
           const uint32_t p0 = (uint32_t)rp;
           int rq = rp;
           uint32_t v;
-#if SBAM_RWIN
           const uint32_t kind = tsym(L, wA, wB, rq, st4, v);
-#else
-          const uint32_t kind = wsym(wp, L, rq, st4, v);
-#endif
           const bool outp = rq > pend;
           const bool stp = live && (kind == K_SPEC || outp);
           if (__builtin_amdgcn_ballot_w64(stp) != 0) {  // rare: record the stop (exit in the literal state | kind) and decode on
@@ -1420,14 +1328,12 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
             go = (stp && outp) ? false : go;
           }
           rp = live ? rq : rp;
-#if SBAM_RWIN
           {
             const bool adv = (((uint32_t)rp ^ p0) >> 5) != 0u;
             wA = adv ? wB : wA;
             wB = adv ? wC : wB;
             wC = win_at(wp, rp)[2];
           }
-#endif
           const bool cnt = live && !stp;
           if constexpr (sj >= 0) {  // the token (a committed step j is token j of the path: no stop before it)
             if constexpr ((sj & 1) == 0) {
@@ -1569,9 +1475,6 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         }
       }
       WMARK(4);
-      // the next window's start (the next round's, or the next block header's) is known now
-      const int next_wq = (f < 64 ? (int)(uni((uint32_t)__shfl(res.exit, f)) >> 10)
-                                  : (int)(uni((uint32_t)__shfl(nxt, 63)) >> 10)) >> 7 << 2;
       // lanes 0..f carry the true path (f: the lane whose segment ends the deflate block, or 64)
       const bool act = lane <= f;
 #ifdef SBAM_WAVE_STATS
@@ -1623,12 +1526,6 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       bool tail = false;
       uint32_t tail_ti = 0, tail_st = 0;
       uint32_t r_lo = 0, r_hi = 0, r_tb = 0;  // register tokens k in [r_lo, r_hi) go to token index r_tb + k
-#if SBAM_TR_PIN == 1
-      // every register token in a VGPR before the first token store: phase A spills a few of them, and a reload
-      // issued after stores waits for all of them (one in-order vmcnt: four store drains per round otherwise)
-      static_assert(kTR == 80, "one asm operand per register token dword");
-      asm volatile("" : "+v"(tr[0]), "+v"(tr[1]), "+v"(tr[2]), "+v"(tr[3]), "+v"(tr[4]), "+v"(tr[5]), "+v"(tr[6]), "+v"(tr[7]), "+v"(tr[8]), "+v"(tr[9]), "+v"(tr[10]), "+v"(tr[11]), "+v"(tr[12]), "+v"(tr[13]), "+v"(tr[14]), "+v"(tr[15]), "+v"(tr[16]), "+v"(tr[17]), "+v"(tr[18]), "+v"(tr[19]), "+v"(tr[20]), "+v"(tr[21]), "+v"(tr[22]), "+v"(tr[23]), "+v"(tr[24]), "+v"(tr[25]), "+v"(tr[26]), "+v"(tr[27]), "+v"(tr[28]), "+v"(tr[29]), "+v"(tr[30]), "+v"(tr[31]), "+v"(tr[32]), "+v"(tr[33]), "+v"(tr[34]), "+v"(tr[35]), "+v"(tr[36]), "+v"(tr[37]), "+v"(tr[38]), "+v"(tr[39]));
-#endif
       if (act) {
         uint32_t start = __shfl_up(nxt, 1);
         if (lane == 0) start = S;
@@ -1658,17 +1555,10 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         r_lo = lo;
         r_hi = hi;
         r_tb = tb;
-#if SBAM_TR_PIN == 2
         static_assert(kTR == 80, "one asm operand per register token dword");
         // (one statement: the spilled ones are reloaded together, one wait)
         asm volatile("" : "+v"(tr[0]), "+v"(tr[1]), "+v"(tr[2]), "+v"(tr[3]), "+v"(tr[4]), "+v"(tr[5]), "+v"(tr[6]), "+v"(tr[7]), "+v"(tr[8]), "+v"(tr[9]), "+v"(tr[10]), "+v"(tr[11]), "+v"(tr[12]), "+v"(tr[13]), "+v"(tr[14]), "+v"(tr[15]), "+v"(tr[16]), "+v"(tr[17]), "+v"(tr[18]), "+v"(tr[19]), "+v"(tr[20]), "+v"(tr[21]), "+v"(tr[22]), "+v"(tr[23]), "+v"(tr[24]), "+v"(tr[25]), "+v"(tr[26]), "+v"(tr[27]), "+v"(tr[28]), "+v"(tr[29]), "+v"(tr[30]), "+v"(tr[31]), "+v"(tr[32]), "+v"(tr[33]), "+v"(tr[34]), "+v"(tr[35]), "+v"(tr[36]), "+v"(tr[37]), "+v"(tr[38]), "+v"(tr[39]));
-#endif
-#ifndef SBAM_DUMP_REPS  // (diagnostic: the register tokens stored this many times, to price the stores)
-#define SBAM_DUMP_REPS 1
-#endif
-#pragma unroll 1
-        for (int rep_ = 0; rep_ < SBAM_DUMP_REPS; rep_++)
-        if (!SBAM_CDUMP) {
+        {
           // 16-B stores (4-B aligned: a 2-B head when tb is odd), dwords and 2-B halves where the run starts or ends
           // inside a chunk — a lane's run is contiguous, so 8 tokens per store instruction instead of one (every
           // store instruction writes 64 lanes' separate lines)
@@ -1713,8 +1603,6 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         tail_st = lo <= (uint32_t)kTR ? stR : rjP << 10;
         tail_ti = lo <= (uint32_t)kTR ? tb + kTR : ti;
       }
-      // the register tokens are stored: their VGPRs take the next window's loads, which the tail decode hides
-      if (SBAM_WPRE & 1) pre.fetch(base, base_dw, next_wq, lim_dw);
       if (tail) {
         uint32_t st4 = (tail_st >> 7) & 4u, ti = tail_ti;
         int rp = (int)(tail_st >> 10);
@@ -1727,86 +1615,9 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
           ti++;
         }
       }
-#if !SBAM_CDUMP
       (void)r_lo;
       (void)r_hi;
       (void)r_tb;
-#else
-      // the register tokens leave through LDS: staged in the (now free) window 2048 tokens at a time, then stored as
-      // whole, 16-B aligned chunks by consecutive lanes (64 lanes x 16 B contiguous per store instruction instead of
-      // 64 lanes' separate runs); a chunk not entirely made of staged tokens (the round's edges, re-decoded
-      // stretches, which were stored directly) is stored token by token
-      {
-        __syncthreads();  // every lane's decodes are done with the window
-        uint16_t *stg = reinterpret_cast<uint16_t *>(L.win);  // [2048]
-        uint32_t *vld = L.win + 1024;                          // [64]: bit t = token P0 + t staged
-        const int T0 = ntok & ~7, T1 = ntok + (int)tot_tok;
-        const uint32_t par = r_tb & 1u;
-        auto dw = [&](auto Q) {  // register dword q: tokens k = par + 2q, par + 2q + 1
-          constexpr int q = decltype(Q)::value;
-          const uint32_t nx = q + 1 < kTR / 2 ? tr[q + 1 < kTR / 2 ? q + 1 : q] : 0u;
-          return par ? __builtin_amdgcn_alignbit(nx, tr[q], 16) : tr[q];
-        };
-        for (int P0 = T0; P0 < T1; P0 += 2048) {
-          vld[lane] = 0u;
-          __syncthreads();
-          const int ka = max((int)r_lo, P0 - (int)r_tb), kb = min((int)r_hi, P0 + 2048 - (int)r_tb);
-          if (ka < kb) {
-            // staging dword of register dword q: (r_tb + par + 2q - P0) / 2 = sd0 + q
-            const int sd0 = ((int)r_tb + (int)par - P0) >> 1;
-            uint32_t *sw = reinterpret_cast<uint32_t *>(stg);
-            if (par && ka == 0) stg[r_tb - P0] = (uint16_t)tr[0];  // token 0 alone in the high half of its dword
-            sfor<0, kTR / 8>([&](auto C) {
-              constexpr int c = decltype(C)::value;
-              const int t0 = (int)par + 8 * c;
-              if (t0 + 8 > ka && t0 < kb) {
-                const uint32_t a0 = dw(std::integral_constant<int, 4 * c>{}), a1 = dw(std::integral_constant<int, 4 * c + 1>{});
-                const uint32_t a2 = dw(std::integral_constant<int, 4 * c + 2>{}), a3 = dw(std::integral_constant<int, 4 * c + 3>{});
-                if (t0 >= ka && t0 + 8 <= kb) {
-                  sw[sd0 + 4 * c] = a0;
-                  sw[sd0 + 4 * c + 1] = a1;
-                  sw[sd0 + 4 * c + 2] = a2;
-                  sw[sd0 + 4 * c + 3] = a3;
-                } else {
-                  const uint32_t a[4] = {a0, a1, a2, a3};
-#pragma unroll
-                  for (int k = 0; k < 4; k++) {
-                    const int u0 = t0 + 2 * k;
-                    const bool in0 = u0 >= ka && u0 < kb, in1 = u0 + 1 >= ka && u0 + 1 < kb;
-                    uint16_t *ph = reinterpret_cast<uint16_t *>(sw + sd0 + 4 * c + k);
-                    if (in0 && in1) sw[sd0 + 4 * c + k] = a[k];
-                    else if (in0) ph[0] = (uint16_t)a[k];
-                    else if (in1) ph[1] = (uint16_t)(a[k] >> 16);
-                  }
-                }
-              }
-            });
-            // staged flags of tokens [r_tb + ka - P0, r_tb + kb - P0)
-            const int fa = (int)r_tb + ka - P0, fb = (int)r_tb + kb - P0;
-            for (int w = fa >> 5; w <= (fb - 1) >> 5; w++) {
-              const int lo32 = max(fa - 32 * w, 0), hi32 = min(fb - 32 * w, 32);
-              const uint32_t m = (hi32 >= 32 ? ~0u : (1u << hi32) - 1u) & ~((1u << lo32) - 1u);
-              atomicOr(vld + w, m);
-            }
-          }
-          __syncthreads();
-#pragma unroll
-          for (int i = 0; i < 4; i++) {
-            const int j = lane + 64 * i, t = P0 + 8 * j;
-            if (t < T1) {
-              const uint32_t m = (vld[j >> 2] >> (8 * (j & 3))) & 0xffu;
-              if (m == 0xffu) {
-                *reinterpret_cast<uint4 *>(reg + 2 * (int64_t)t) = *reinterpret_cast<const uint4 *>(stg + 8 * j);
-              } else if (m) {
-                for (int k = 0; k < 8; k++)
-                  if ((m >> k) & 1u) reinterpret_cast<uint16_t *>(reg)[t + k] = stg[8 * j + k];
-              }
-            }
-          }
-          __syncthreads();
-        }
-      }
-#endif
       WMARK(28);
       out += (int)tot_byt;
       ntok += (int)tot_tok;
@@ -1850,21 +1661,8 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
 // A block's LZ77 window never leaves the chip except for the far copies; HBM sees the words once and the output
 // once.  (Round 2; the round-1 design ran one lane per block with the window in HBM and was bound by the memory
 // side: 16.5x the output bytes per launch.)
-// SBAM_FAR_DEFER=1: far copies wait until the first pending match is far, so their loads overlap the near rounds.
-// Round 4 A/B at 10 GB: 41.2 ms with, 38.7 ms without (the deferred far copies added rounds).  (Also tried in round
-// 4: four tokens per lane per step, to halve the per-step overhead: 46.2 ms deferred / 42.1 not — slower.)
-#ifndef SBAM_FAR_DEFER
-#define SBAM_FAR_DEFER 0
-#endif
-#ifndef SBAM_RES_FARWAIT
-#define SBAM_RES_FARWAIT 1
-#endif
-#ifndef SBAM_RES_EARLYFLUSH
-#define SBAM_RES_EARLYFLUSH 1
-#endif
-#ifndef SBAM_RES_TOKWAIT
-#define SBAM_RES_TOKWAIT 1
-#endif
+// (Round 4, measured and dropped: far copies deferred until the first pending match is far, 41.2 vs 38.7 ms at 10 GB
+// — the deferral added rounds; four tokens per lane per step, 46.2 / 42.1 ms.)
 namespace rs {
 constexpr int kSpan = 1024;   // a chunk's words start within kSpan bytes of its base
 constexpr int kFlush = 1024;  // output bytes per group store (64 lanes x 16 B)
@@ -1945,9 +1743,7 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
   bool toofar = false;                            // a distance past the block's first byte (zlib: data error)
   // lane i holds tokens tp + 2i and tp + 2i + 1, and sees tp + 2i + 2 (the distance of a length in its second)
   uint32_t ta = tk[2 * lane], tb = tk[2 * lane + 1], tn = tk[2 * lane + 2];
-#if SBAM_RES_TOKWAIT
   asm volatile("" : "+v"(ta), "+v"(tb), "+v"(tn));  // (no token load pending at the loop head, from either edge)
-#endif
 #ifdef SBAM_WAVE_STATS
   uint64_t rs_[8] = {0};
   uint32_t it_ = 0;
@@ -2002,7 +1798,6 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
       }
     }
     RMARK(1);  // literals
-#if SBAM_RES_EARLYFLUSH
     // ---- 4. output of the chunks before this one ([F, B) is final), issued before this step's loads: the stores
     // precede the next step's token loads, so waiting for those never waits for the stores (one in-order vmcnt; a
     // data-dependent store count after the loads made the compiler wait with vmcnt(0))
@@ -2015,7 +1810,6 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
       *reinterpret_cast<uint4 *>(ob + F + 16 * lane) = *reinterpret_cast<const uint4 *>(ring8 + x);
       F += rs::kFlush;
     }
-#endif
     RMARK(2);  // output stores
     // ---- 3b. matches, in rounds
     const int mO = O + (bLen ? nl : 0);
@@ -2034,16 +1828,11 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
       if (Le > 16) pf1 = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(ob + mO - d + 16));
     }
     // the next step's tokens, loaded after the far sources: a wait for a far source need not wait for them
-#if SBAM_RES_TOKWAIT
     // (as raw registers, split only after the rounds: see the end of the step)
     uint32_t w2, n2;
     __builtin_memcpy(&w2, tk + tp2 + 2 * lane, 4);
     n2 = tk[tp2 + 2 * lane + 2];
-#else
-    const uint32_t ta2 = tk[tp2 + 2 * lane], tb2 = tk[tp2 + 2 * lane + 1], tn2 = tk[tp2 + 2 * lane + 2];
-#endif
     RMARK(3);  // match setup, far prefetch, next tokens issued
-    const uint64_t farm = __ballot(mt && far);
     uint64_t pend = __ballot(mt);
     const uint64_t below = (1ull << lane) - 1ull;
     const int mEnd = mO + Le;
@@ -2056,7 +1845,6 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
       const int jn = pb ? 63 - __clzll((long long)pb) : lane;
       const int endj = __shfl(mEnd, jn);
       uint64_t ready = pend & __ballot(srcEnd <= fr || pb == 0 || endj <= mO - d);
-      if (SBAM_FAR_DEFER && !((farm >> f) & 1ull)) ready &= ~farm;
       if ((ready >> lane) & 1ull) {
         int done = 0, deff = d;
         while (done < Le) {
@@ -2067,7 +1855,6 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
           const int src = mO + done - deff;
           uint32_t v0, v1, v2, v3;
           if (far) {  // below the flushed mark: unaligned 16-B loads, past this CU's L1 (nt)
-#if SBAM_RES_FARWAIT
             // each path waits for its own source here (the prefetched ones: vmcnt(2), the next step's two token
             // loads may stay in flight): merged with the near path's registers, the compiler waited with vmcnt(0)
             // after the join, so every near copy also waited for the next step's tokens
@@ -2080,11 +1867,6 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
               v0 = x.x; v1 = x.y; v2 = x.z; v3 = x.w;
               asm volatile("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));
             }
-#else
-            u32x4 x = done == 0 ? pf0 : pf1;
-            if (done >= 32) x = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(ob + src));
-            v0 = x.x; v1 = x.y; v2 = x.z; v3 = x.w;
-#endif
           } else {
             const uint32_t xs = (Gr + (uint32_t)src) & G::kMask, qs = xs >> 2, ss = xs & 3u;
             const uint32_t *p = ring + qs;  // (qs + 4 < kDw + kMirror: the mirror covers the wrap)
@@ -2127,19 +1909,6 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
     }
     RMARK(4);  // rounds
     B = E;
-#if !SBAM_RES_EARLYFLUSH
-    // ---- 4. output
-    if (!head && B >= F0) {  // the block's first partial 16-B chunk (shared with the previous block)
-      if (lane < F0) ob[lane] = ring8[(Gr + (uint32_t)lane) & G::kMask];
-      head = true;
-    }
-    while (B - F >= rs::kFlush) {
-      const uint32_t x = (Gr + (uint32_t)(F + 16 * lane)) & G::kMask;  // 16-B aligned
-      *reinterpret_cast<uint4 *>(ob + F + 16 * lane) = *reinterpret_cast<const uint4 *>(ring8 + x);
-      F += rs::kFlush;
-    }
-#endif
-#if SBAM_RES_TOKWAIT
     // the wait for the next step's tokens, here: the compiler otherwise split them right after the loads (waiting
     // there), or let this step's last use of tn wait after the stores (one in-order vmcnt)
     asm volatile("" : "+v"(w2), "+v"(n2));
@@ -2149,11 +1918,6 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
     RMARK(5);  // the wait for the next tokens
 #ifdef SBAM_WAVE_STATS
     rs_[6]++;  // steps
-#endif
-#else
-    ta = ta2;
-    tb = tb2;
-    tn = tn2;
 #endif
     tp = tp2;
   }

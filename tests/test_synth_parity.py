@@ -49,19 +49,20 @@ def test_synthetic_every_offset_and_counts(synth_file):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["many_contigs", "reads_to_check_0"])
+@pytest.mark.parametrize("case", ["many_contigs", "many_contigs_short", "reads_to_check_0"])
 def test_counts_general_paths(synth_file, case):
-    """The bit-sliced interior pass (k_check_bits) needs R > 0 and the contig lengths in LDS (n_ref <= 4096); the
-    other cases run the general k_check<MODE_COUNTS, 0> over every tile.  Both against the oracle: 5000 contigs
-    (the 84 real ones, then 4916 more, so refIdx values up to 4999 become in-range) and reads_to_check = 0."""
+    """Past the bit-sliced interior pass's LDS table of contig lengths (n_ref > 4096: the rare length probes read the
+    device table, round 5) and with reads_to_check = 0 (the general k_check<MODE_COUNTS, 0> over every tile), against
+    the oracle: 5000 contigs (the 84 real ones, then 4916 more, so refIdx values up to 4999 become in-range; "short":
+    lengths 1-999, so refPos > length fires on many of them) and R = 0."""
     import sbam
     s, data, o = synth_file
     R = 0 if case == "reads_to_check_0" else 10
     lens, nref = o.lens, o.nref
     try:
-        if case == "many_contigs":
+        if case.startswith("many_contigs"):
             rng = np.random.default_rng(7)
-            extra = rng.integers(1, 1 << 31, 5000 - o.nref).astype(np.int64)
+            extra = rng.integers(1, 1000 if case.endswith("short") else 1 << 31, 5000 - o.nref).astype(np.int64)
             o.lens = np.zeros(1 << 16, np.int64)
             o.lens[:nref] = lens[:nref]
             o.lens[nref:5000] = extra
