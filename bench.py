@@ -293,10 +293,12 @@ def main():
         pipe = sdist.WindowPipe(wplans_of(W), stage_synth, split_size, s.contig_lengths, local, run_window,
                                 prefetch=True)
 
+    gathered = {}
+
     def step():
         res, ms = merge([run_window(shard)] if W == 1 else pipe.step())
         if world > 1 and args.workload == "full-check":
-            sdist.gather_results(res, plans, device=cdev)
+            gathered["all"] = sdist.gather_results(res, plans, device=cdev)
         return res, ms
 
     def sync():
@@ -344,6 +346,15 @@ def main():
         tot_succ, tot_rec, n_bad = counts["n_success"], n_rec, int(not ok_local)
     parity = {"records": tot_rec, "expected_records": s.n_records, "checker_true": tot_succ,
               "ok": bool(tot_rec == s.n_records and tot_succ == s.n_records and n_bad == 0)}
+    # digests of the whole file's full-check Counts and split rows (first Pos, non-empty, records per split), whatever
+    # the sharding: an N-rank run and a one-process run over the same file must print the same ones
+    if args.workload == "full-check":
+        import hashlib
+        parts = gathered["all"] if world > 1 else [res]
+        rows = np.concatenate([np.stack([p.first_block_pos, p.first_offset, p.nonempty, p.n_records]).T.ravel()
+                               for p in parts]).astype(np.int64)
+        parity["digest"] = {"counts": hashlib.sha1(parts[0].counts.astype(np.int64).tobytes()).hexdigest()[:16],
+                            "splits": hashlib.sha1(rows.tobytes()).hexdigest()[:16], "n_splits": int(rows.size // 4)}
     if not parity["ok"]:
         log(f"[rank {rank}] PARITY PROPERTY FAILED: {parity}")
 
