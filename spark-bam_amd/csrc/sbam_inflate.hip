@@ -764,9 +764,6 @@ constexpr int kWarm = 640;
 // 55.0 ms; the next window prefetched into registers during phase C or the table build, 44.3 ms; the register tokens
 // pinned before phase C's re-decode instead of after it.)
 constexpr int kTR = 80;
-#ifndef SBAM_PAIR
-#define SBAM_PAIR 1
-#endif
 static_assert(kTR % 2 == 0 && kTR <= kCp * kCpSteps, "register tokens come from the unrolled checkpoint steps");
 static_assert(kTR % kCpSteps == 0, "the state after step kTR (stR) is saved at a checkpoint");
 constexpr int kScratchDw = 256;    // window tail that doubles as header / table-build scratch
@@ -1285,129 +1282,15 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
             st4 = (S >> 7) & 4u;
             pl = S & 511u;
           }
-#if SBAM_PAIR
-          // two symbols per iteration, the second taken while the first ends before the segment start
-          while (rp < seg_start) {
-            uint32_t v1, v2;
-            int rq = rp;
-            const uint32_t k1 = wsym(wp, L, rq, st4, v1);
-            const uint32_t st4a = k1 == K_LEN ? 4u : 0u, pla = k1 == K_LEN ? v1 - 253u : pl;
-            const int r1 = rq;
-            const uint32_t k2 = wsym(wp, L, rq, st4a, v2);
-            const bool t2 = r1 < seg_start;
-            rp = t2 ? rq : r1;
-            pl = (t2 && k2 == K_LEN) ? v2 - 253u : pla;
-            st4 = t2 ? (k2 == K_LEN ? 4u : 0u) : st4a;
-          }
-#else
           while (rp < seg_start) {
             uint32_t v;
             const uint32_t kind = wsym(wp, L, rp, st4, v);
             pl = kind == K_LEN ? v - 253u : pl;
             st4 = kind == K_LEN ? 4u : 0u;
           }
-#endif
         }
         WMARK(13);
         entry = ((uint32_t)rp << 10) | (st4 << 7) | pl;
-#if SBAM_PAIR
-        // Two symbols per step (round 5): the second is decoded with the state the first leaves (a distance after a
-        // length, else a literal/length), so symbol i of the path is still register token i (step j: both halves of
-        // tr[j]) and the per-step bookkeeping — liveness, the stop ballot, the window, the counts — is paid once per
-        // two symbols.  The dependent chain per symbol is unchanged.  The window dwords W .. W + 3 of the reader
-        // (W = rp >> 5) are in registers: a symbol is at most 28 bits, so a step moves the reader by at most 56 bits
-        // (two dwords), and dwords W + 2, W + 3 of the new reader are loaded a whole step before use.
-        uint32_t wA, wB, wC, wD;
-        {
-          const lds_u32 q = win_at(wp, rp);
-          wA = q[0];
-          wB = q[1];
-          wC = q[2];
-          wD = q[3];
-        }
-        // predicated: a lane that is done (stopped out of the data, or past its segment) decodes the same symbols
-        // again and commits nothing, so the steps need no exec-mask branches.  ST: the step's index when its tokens
-        // go to tr (tokens 2 ST, 2 ST + 1), else -1
-        auto step = [&](auto ST) {
-          constexpr int sj = decltype(ST)::value;
-          const bool live1 = go && rp < seg_end;
-          const uint32_t p0 = (uint32_t)rp;
-          int rq = rp;
-          uint32_t v1, v2;
-          const uint32_t k1 = tsym(L, wA, wB, rq, st4, v1);
-          const int r1 = rq;
-          const bool out1 = r1 > pend;
-          const bool stp1 = live1 && (k1 == K_SPEC || out1);
-          const bool c1 = live1 && !stp1, cl1 = c1 && k1 == K_LEN;
-          const uint32_t st4b = cl1 ? 4u : 0u;
-          const bool a1 = (((uint32_t)r1 ^ p0) >> 5) != 0u;
-          const uint32_t k2 = tsym(L, a1 ? wB : wA, a1 ? wC : wB, rq, st4b, v2);
-          const bool live2 = live1 && !(stp1 && out1) && r1 < seg_end;
-          const bool out2 = rq > pend;
-          const bool stp2 = live2 && (k2 == K_SPEC || out2);
-          const uint32_t b1 = c1 ? (k1 == K_LEN ? v1 - 253u : k1 == K_LIT ? 1u : 0u) : 0u;
-          if (__builtin_amdgcn_ballot_w64(stp1 || stp2) != 0) {  // rare: record the stops (in order) and decode on
-            const uint32_t ek1 = ((uint32_t)r1 << 10) | (uint32_t)(out1 ? ST_OUT : v1 == 0 ? ST_EOB : ST_ERR);
-            const uint32_t ek2 = ((uint32_t)rq << 10) | (uint32_t)(out2 ? ST_OUT : v2 == 0 ? ST_EOB : ST_ERR);
-            const uint32_t cn1 = tokA | (bytA << 12), cn2 = (tokA + (c1 ? 1u : 0u)) | ((bytA + b1) << 12);
-            // stop 1 takes slot nst, stop 2 the slot after it
-            const int n2 = nst + (stp1 ? 1 : 0);
-            const bool w11 = stp1 && nst == 0, w12 = stp1 && nst == 1;
-            const bool w21 = stp2 && n2 == 0, w22 = stp2 && n2 == 1;
-            s1p = w11 ? p0 : w21 ? (uint32_t)r1 : s1p;
-            s1e = w11 ? ek1 : w21 ? ek2 : s1e;
-            s1c = w11 ? cn1 : w21 ? cn2 : s1c;
-            s2p = w12 ? p0 : w22 ? (uint32_t)r1 : s2p;
-            s2e = w12 ? ek1 : w22 ? ek2 : s2e;
-            s2c = w12 ? cn1 : w22 ? cn2 : s2c;
-            nst = n2 + (stp2 ? 1 : 0);
-            go = ((stp1 && out1) || (stp2 && out2)) ? false : go;
-          }
-          rp = live2 ? rq : live1 ? r1 : rp;
-          {
-            const uint32_t d = ((uint32_t)rp >> 5) - (p0 >> 5);  // 0, 1 or 2 dwords
-            const uint32_t nA = d == 0u ? wA : d == 1u ? wB : wC, nB = d == 0u ? wB : d == 1u ? wC : wD;
-            wA = nA;
-            wB = nB;
-            const lds_u32 q = win_at(wp, rp);
-            wC = q[2];
-            wD = q[3];
-          }
-          if constexpr (sj >= 0) tr[sj] = (v1 & 0xffffu) | (v2 << 16);
-          // selects and carry-in adds only (no exec-mask branches): counts and the pending length.  (zlib's
-          // "invalid distance too far back" is the resolver's test: k_inflate_resolve hands such a block back.)
-          const bool c2 = live2 && !stp2, cl2 = c2 && k2 == K_LEN;
-          const uint32_t b2 = c2 ? (k2 == K_LEN ? v2 - 253u : k2 == K_LIT ? 1u : 0u) : 0u;
-          tokA += (c1 ? 1u : 0u) + (c2 ? 1u : 0u);
-          bytA += b1 + b2;
-          pl = cl2 ? v2 - 253u : cl1 ? v1 - 253u : pl;
-          st4 = live2 ? (cl2 ? 4u : 0u) : live1 ? st4b : st4;
-        };
-        static_assert(kCpSteps % 2 == 0 && kTR % 2 == 0, "checkpoints and register tokens at step boundaries");
-        // checkpoints every kCpSteps symbols (wave-uniform, so a record costs no divergent branch): the lane's
-        // position if it is at a literal/length boundary
-        sfor<0, kCp>([&](auto J) {
-          constexpr int jj = decltype(J)::value;
-          const bool live = go && rp < seg_end;
-          cp[jj] = (live && st4 == 0) ? (uint32_t)rp : ~0u;
-          cc[jj] = tokA | (bytA << 12);
-          if (__ballot(live) != 0) {
-            if constexpr (jj * kCpSteps < kTR) {
-              sfor<0, kCpSteps / 2>([&](auto K) {
-                constexpr int sj = jj * kCpSteps / 2 + decltype(K)::value;
-                step(std::integral_constant<int, (2 * sj < kTR ? sj : -1)>{});
-              });
-            } else {
-#pragma unroll 2
-              for (int k = 0; k < kCpSteps / 2; k++) step(std::integral_constant<int, -1>{});
-            }
-          }
-          if constexpr ((jj + 1) * kCpSteps == kTR) {
-            stR = ((uint32_t)rp << 10) | (st4 << 7) | pl;
-            bytR = bytA;
-          }
-        });
-#else
         // the window dwords W, W + 1, W + 2 of the reader (W = rp >> 5) in registers: a symbol is at most 28 bits,
         // so the next reader is in W or W + 1, and dword W + 2 of the new reader is loaded a whole step before use
         // (one LDS round trip less on a step's dependent chain: root entry, sub-table entry; decode 46.0 → 45.7 ms.
@@ -1491,7 +1374,6 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
             bytR = bytA;
           }
         });
-#endif
         while (__ballot(go && rp < seg_end) != 0) step(std::integral_constant<int, -1>{});
         exitEnd = ((uint32_t)rp << 10) | (st4 << 7) | pl;
       }
