@@ -1243,7 +1243,16 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
     if (!wave_build<false>(L, 0, hlit, kLitSubOff, kLitSub)) { ok = false; break; }
     WMARK(1);
 
-    // ---- data rounds: 64 segments of kK bits per round
+    // ---- data rounds: 64 segments of kK bits per round.  The last deflate block (BFINAL) runs to the payload's end,
+    // so its rounds are sized to it: the same number of rounds with segments of kS <= kK bits spread evenly, instead
+    // of a last round whose lanes past the end decode nothing of use (zlib's last block of a BGZF block is its last
+    // ~7 %, one round of ~7 per block, 40 % used)
+    int kS = kK;
+    if (fin) {
+      const int left = pend - h.pos, nr = (left + 64 * kK - 1) / (64 * kK);
+      kS = nr > 0 ? min(kK, max(32, (((left + 64 * nr - 1) / (64 * nr)) + 31) & ~31)) : kK;
+      kS = uni(kS);
+    }
     uint32_t S = (uint32_t)h.pos << 10;  // round start: pos << 10 | state << 9 | pending match length
     for (;;) {
       const int Sp = (int)(S >> 10);
@@ -1252,8 +1261,8 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       const uint32_t *wp = L.win - (wq >> 5);  // wp[pos >> 5]: the staged dword holding bit pos
       WMARK(2);
       WADD(6, 1);
-      const int seg_start = lane == 0 ? Sp : Sp + lane * kK;
-      const int seg_end = Sp + (lane + 1) * kK;
+      const int seg_start = lane == 0 ? Sp : Sp + lane * kS;
+      const int seg_end = Sp + (lane + 1) * kS;
       // ---- phase A: every lane decodes its segment from a guessed start (lane 0: the true one)
       uint32_t cp[kCp], cc[kCp];  // checkpoints: position (literal/length state) and tok | byt << 12 there
       sfor<0, kCp>([&](auto I) {
