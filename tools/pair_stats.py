@@ -61,40 +61,45 @@ def decode(payload):
         if fin: break
     return out
 
-s = synth.SynthBam(tile_mb=8.0)
-raw = s.bytes().tobytes()
-pos = 0; blocks=[]
-while pos + 18 <= len(raw):
-    bsize = raw[pos+16] | (raw[pos+17]<<8); end = pos+bsize+1
-    isz = int.from_bytes(raw[end-4:end],'little')
-    if isz: blocks.append(raw[pos+18:end-8])
-    pos = end
-print("blocks", len(blocks))
-tot = {'sym':0,'lit':0,'bits':0,'steps9':0,'steps10':0,'steps11':0,'steps9x':0, 'dblocks':0}
-for b in blocks[20:60]:
-    for blk in decode(b):
-        tot['dblocks']+=1
-        syms=[x for x in blk]
-        tot['sym']+=len(syms); tot['lit']+=sum(1 for k,_,_ in syms if k==0)
-        tot['bits']+=sum(l+x for _,l,x in syms)
-        for R,key in ((9,'steps9'),(10,'steps10'),(11,'steps11')):
+def main():
+    s = synth.SynthBam(tile_mb=8.0)
+    raw = s.bytes().tobytes()
+    pos = 0; blocks=[]
+    while pos + 18 <= len(raw):
+        bsize = raw[pos+16] | (raw[pos+17]<<8); end = pos+bsize+1
+        isz = int.from_bytes(raw[end-4:end],'little')
+        if isz: blocks.append(raw[pos+18:end-8])
+        pos = end
+    print("blocks", len(blocks))
+    tot = {'sym':0,'lit':0,'bits':0,'steps9':0,'steps10':0,'steps11':0,'steps9x':0, 'dblocks':0}
+    for b in blocks[20:60]:
+        for blk in decode(b):
+            tot['dblocks']+=1
+            syms=[x for x in blk]
+            tot['sym']+=len(syms); tot['lit']+=sum(1 for k,_,_ in syms if k==0)
+            tot['bits']+=sum(l+x for _,l,x in syms)
+            for R,key in ((9,'steps9'),(10,'steps10'),(11,'steps11')):
+                i=0; st=0
+                while i<len(syms):
+                    k,l,x=syms[i]
+                    if k==0 and i+1<len(syms) and syms[i+1][0]==0 and l+syms[i+1][1]<=R: i+=2
+                    else: i+=1
+                    st+=1
+                tot[key]+=st
+            # 9-bit root: also lit+len(with no extra bits), len(no extra)+... and len+dist if total<=9
             i=0; st=0
             while i<len(syms):
                 k,l,x=syms[i]
-                if k==0 and i+1<len(syms) and syms[i+1][0]==0 and l+syms[i+1][1]<=R: i+=2
-                else: i+=1
-                st+=1
-            tot[key]+=st
-        # 9-bit root: also lit+len(with no extra bits), len(no extra)+... and len+dist if total<=9
-        i=0; st=0
-        while i<len(syms):
-            k,l,x=syms[i]
-            if i+1<len(syms):
-                k2,l2,x2=syms[i+1]
-                if k==0 and k2 in (0,) and l+l2<=9: i+=2; st+=1; continue
-                if k==1 and k2==2 and l+x+l2<=9: i+=2; st+=1; continue
-            i+=1; st+=1
-        tot['steps9x']+=st
-print(tot)
-print("bits/sym %.2f lit frac %.3f" % (tot['bits']/tot['sym'], tot['lit']/tot['sym']))
-for k in ('steps9','steps10','steps11','steps9x'): print(k, "%.3f"%(tot[k]/tot['sym']))
+                if i+1<len(syms):
+                    k2,l2,x2=syms[i+1]
+                    if k==0 and k2 in (0,) and l+l2<=9: i+=2; st+=1; continue
+                    if k==1 and k2==2 and l+x+l2<=9: i+=2; st+=1; continue
+                i+=1; st+=1
+            tot['steps9x']+=st
+    print(tot)
+    print("bits/sym %.2f lit frac %.3f" % (tot['bits']/tot['sym'], tot['lit']/tot['sym']))
+    for k in ('steps9','steps10','steps11','steps9x'): print(k, "%.3f"%(tot[k]/tot['sym']))
+
+
+if __name__ == "__main__":
+    main()

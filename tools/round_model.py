@@ -1,9 +1,18 @@
-import sys, os, math
-sys.path[:0] = ["/root/repo/tools", "/root/repo/spark-bam_amd"]
-import numpy as np
-import synth
-exec(open("/root/repo/tools/pair_stats.py").read().split("s = synth.SynthBam")[0])
-from sbam.dist import _CL_ORDER, _LEN_EXTRA, _DIST_EXTRA
+#!/usr/bin/env python3
+"""Round model of k_inflate_wave on the synthetic BAM (round 5): per BGZF block its DEFLATE blocks
+(bit extents, symbols), the decoder's rounds (64 lanes x 544-bit segments, a 96-symbol warm-up per lane and round)
+and the lane-steps they cost, with and without the last (BFINAL) block's rounds sized to the payload's end; and how
+zlib splits a BGZF payload (non-final blocks of ~16K zlib symbols = the first ~93 % of the bits).
+Output: profiles/r05/round_model.log."""
+import math
+import os
+import sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "tools"), os.path.join(ROOT, "spark-bam_amd")]
+import numpy as np  # noqa: E402
+import synth  # noqa: E402
+from pair_stats import huff  # noqa: E402
+from sbam.dist import _CL_ORDER, _LEN_EXTRA, _DIST_EXTRA  # noqa: E402
 
 def dblocks(payload):
     """(final, header_start_bit, data_start_bit, end_bit, nsym) per deflate block"""
