@@ -885,14 +885,15 @@ SB_DEV bool wave_build(WaveLds &L, int off, int nsym, int suboff, int subcap) {
   // sorted[canonical index] = symbol: a symbol's rank among the equal-length symbols below it, 64 at a time
   int32_t run[16];
   sfor<1, 16>([&](auto I) { run[decltype(I)::value] = 0; });
-  const uint64_t lt = (1ull << lane) - 1ull;
   for (int c0 = 0; c0 < nsym; c0 += 64) {
     const int s = c0 + lane;
     const uint32_t l = s < nsym ? lens[off + s] : 0u;
     sfor<1, 16>([&](auto I) {
       constexpr int ll = decltype(I)::value;
       const uint64_t m = __ballot(l == (uint32_t)ll);
-      if (l == (uint32_t)ll) sorted[off + offs[ll] + run[ll] + __popcll(m & lt)] = (uint16_t)s;
+      // (the lanes of m below this one by mbcnt: a (1 << lane) - 1 mask can be spilled and reloaded per length)
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (l == (uint32_t)ll) sorted[off + offs[ll] + run[ll] + (int)below] = (uint16_t)s;
       run[ll] += __popcll(m);
     });
   }

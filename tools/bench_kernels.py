@@ -54,6 +54,12 @@ def main():
                 tt[k].append(f.kernel_ms(k))
         for k in tt:
             ms[k] = round(float(np.median(tt[k])), 3)
+        out["inflate_fallbacks"] = int(f.inflate_fallbacks())  # blocks the exact decoder took
+        if hasattr(f.L, "sbam_debug_inflate_pieced"):  # blocks whose first DEFLATE block went through the lane regions
+            import ctypes
+            n = ctypes.c_int64(0)
+            if f.L.sbam_debug_inflate_pieced(f.ctx, ctypes.byref(n)) == 0:
+                out["inflate_pieced"] = int(n.value)
     if "check_full" in only:
         timed("check_full", lambda: f.check_full_counts(0, U), "check_full")
         c = f.check_full_counts(0, U)
