@@ -764,6 +764,7 @@ constexpr int kWarm = 640;
 // 55.0 ms; the next window prefetched into registers during phase C or the table build, 44.3 ms; the register tokens
 // pinned before phase C's re-decode instead of after it.)
 constexpr int kTR = 80;
+constexpr int kFirstFrac = 930;  // per mille: a non-final DEFLATE block's rounds are sized to this much of the rest
 static_assert(kTR % 2 == 0 && kTR <= kCp * kCpSteps, "register tokens come from the unrolled checkpoint steps");
 static_assert(kTR % kCpSteps == 0, "the state after step kTR (stR) is saved at a checkpoint");
 constexpr int kScratchDw = 256;    // window tail that doubles as header / table-build scratch
@@ -1248,9 +1249,15 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
     // so its rounds are sized to it: the same number of rounds with segments of kS <= kK bits spread evenly, instead
     // of a last round whose lanes past the end decode nothing of use (zlib's last block of a BGZF block is its last
     // ~7 %, one round of ~7 per block, 40 % used)
+    // A non-final block's end is not known, but zlib's first block of a BGZF payload ends at 92-94 % of its bits
+    // (16383 literals and matches: profiles/r05/round_model.log): its rounds are sized as if it ended at 93 % —
+    // one round fewer-used lanes in the last one (decode 40.3 -> 39.5 ms at 10 GB; 95 %: 39.7, 97 %: 42.0, the
+    // rounds then no longer cover the block; profiles/r05/ab/firstfrac_*.log).  Another structure only changes
+    // how full the rounds are.
     int kS = kK;
-    if (fin) {
-      const int left = pend - h.pos, nr = (left + 64 * kK - 1) / (64 * kK);
+    {
+      const int left = fin ? pend - h.pos : (int)((int64_t)(pend - h.pos) * kFirstFrac / 1000);
+      const int nr = (left + 64 * kK - 1) / (64 * kK);
       kS = nr > 0 ? min(kK, max(32, (((left + 64 * nr - 1) / (64 * nr)) + 31) & ~31)) : kK;
       kS = uni(kS);
     }
