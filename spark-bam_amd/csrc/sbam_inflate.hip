@@ -907,9 +907,15 @@ SB_DEV bool wave_build(WaveLds &L, int off, int nsym, int suboff, int subcap) {
       L.tab[2 * e + DIST] = sym_entry(sorted[off + (int)(v >> (15 - l)) + canon_base<R>(c, l)], l, DIST);
     }
   }
-  // sub-tables: one per root prefix of the codes longer than R, sized by the longest code under that prefix
+  // sub-tables: one per root prefix of the codes longer than R, sized by the longest code under that prefix.  A
+  // lane per prefix lays them out (offset, index bits) and marks its entries' owner; then all lanes fill the
+  // entries, 64 at a time (on the synthetic BAM ~22 literal prefixes of up to 32 entries: a lane per prefix filling
+  // its own ran 32 serial steps of canonical decoding).  Scratch: the window, restaged before the data rounds.
   const uint32_t P0 = c.lim[R] >> (15 - R);
   const int npre = (1 << R) - (int)P0;
+  uint16_t *own = reinterpret_cast<uint16_t *>(L.win);  // [subcap] prefix index of each sub-table entry
+  uint32_t *pinfo = L.win + 256;                           // [npre] offset | index bits << 16
+  static_assert(wd::kLitSub <= 512 && 256 + 512 <= wd::kWinDw - wd::kScratchDw, "sub-table scratch in the window");
   int next = 0;
   for (int j0 = 0; j0 < npre; j0 += 64) {
     const int j = j0 + lane;
@@ -924,13 +930,20 @@ SB_DEV bool wave_build(WaveLds &L, int off, int nsym, int suboff, int subcap) {
     if (j < npre && my + (int)sz <= subcap) {
       L.tab[2 * (__builtin_bitreverse32(P) >> (32 - R)) + DIST] =
           (wd::K_SUBP << 8) | sb | ((uint32_t)(4 * (suboff + my)) << 16);
-      for (uint32_t k = 0; k < sz; k++) {
-        const uint32_t v = (P << (15 - R)) | ((__builtin_bitreverse32(k) >> (32 - sb)) << (15 - R - sb));
-        const uint32_t l = canon_len(c, v);
-        L.tab[suboff + my + (int)k] = sym_entry(sorted[off + (int)(v >> (15 - l)) + canon_base(c, l)], l, DIST);
-      }
+      pinfo[j] = (uint32_t)my | (sb << 16);
+      for (uint32_t k = 0; k < sz; k++) own[my + (int)k] = (uint16_t)j;
     }
     next += (int)__shfl(incl, 63);
+  }
+  __syncthreads();
+  if (next <= subcap) {
+    for (int e = lane; e < next; e += 64) {
+      const int j = own[e];
+      const uint32_t info = pinfo[j], sb = info >> 16, P = P0 + (uint32_t)j, k = (uint32_t)e - (info & 0xffffu);
+      const uint32_t v = (P << (15 - R)) | ((__builtin_bitreverse32(k) >> (32 - sb)) << (15 - R - sb));
+      const uint32_t l = canon_len(c, v);
+      L.tab[suboff + e] = sym_entry(sorted[off + (int)(v >> (15 - l)) + canon_base(c, l)], l, DIST);
+    }
   }
   __syncthreads();
   return next <= subcap;
