@@ -1166,7 +1166,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       }
       __syncthreads();
       WMARK(10);
-      const int total = hlit + hdist;
+      const int total = uni(hlit + hdist);  // (uni: the compiler kept it, and the loop below, in VGPRs)
       int n = 0, p = h.pos;
       uint32_t prev = 0;
       while (n < total) {
@@ -1199,16 +1199,18 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         int o = 0;
         uint64_t chain = 0;
         const int n0 = n;
+        // (o, n and chain pinned to scalar registers: left to the compiler, they lived in VGPRs and every step
+        // went VGPR -> readfirstlane -> readlane -> VGPR under exec-mask bookkeeping)
         while (o < 64 && n < total) {
           const uint32_t in = (uint32_t)__builtin_amdgcn_readlane((int)info, o);
           const uint32_t in2 = (uint32_t)__builtin_amdgcn_readlane((int)info2, o);
-          chain |= 1ull << o;
-          n += (int)((in >> 5) & 255u);
-          const int o1 = o + (int)(in & 31u);
+          chain = uni((uint64_t)(chain | (1ull << o)));
+          n = uni(n + (int)((in >> 5) & 255u));
+          const int o1 = uni(o + (int)(in & 31u));
           if (o1 < 64 && n < total) {
-            chain |= 1ull << o1;
-            n += (int)((in2 >> 5) & 255u);
-            o = o1 + (int)(in2 & 31u);
+            chain = uni((uint64_t)(chain | (1ull << o1)));
+            n = uni(n + (int)((in2 >> 5) & 255u));
+            o = uni(o1 + (int)(in2 & 31u));
           } else {
             o = o1;
           }
