@@ -1123,16 +1123,17 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       uint64_t clp = 0;
       for (int i = 0; i < 19; i++)
         if (i < hclen) clp |= (uint64_t)h.get(L.win, 3) << (3 * kClOrder[i]);
-      // code-length code (must be complete): left-justified 7-bit limits and the symbols in canonical order
+      // code-length code (must be complete): left-justified 7-bit limits and the symbols in canonical order.  Lane s
+      // < 19 holds symbol s's length: the counts per length are ballots, a symbol's canonical rank is a 19-step count
+      // on its own lane (the wave-uniform form was a 19 x 19 compare loop per header)
+      const uint32_t lsym = lane < 19 ? (uint32_t)(clp >> (3 * lane)) & 7u : 0u;
       int left = 1;
       bool over = false;
       uint32_t lim7[8], base7[8], code = 0;
       int acc = 0;
 #pragma unroll
       for (int l = 1; l <= 7; l++) {
-        uint32_t k = 0;
-#pragma unroll
-        for (int s2 = 0; s2 < 19; s2++) k += ((clp >> (3 * s2)) & 7) == (uint64_t)l ? 1u : 0u;
+        const uint32_t k = (uint32_t)__popcll(__ballot(lsym == (uint32_t)l));
         left = 2 * left - (int)k;
         over |= left < 0;
         lim7[l] = (code + k) << (7 - l);
@@ -1143,26 +1144,19 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       if (over || left != 0) { ok = false; break; }
       for (int i = lane; i < 320; i += 64) lens[i] = 0;
       // every lane decodes the code-length symbol at bit b0 + lane: advance, repeat count, value kind
-      uint32_t srt[4] = {0, 0, 0, 0};  // symbols in canonical order, 5 bits each, 6 per dword
+      uint32_t srt[4];  // symbols in canonical order, 5 bits each, 6 per dword
       {
-        uint32_t rank = 0;
+        uint32_t r = 0;
 #pragma unroll
-        for (int s2 = 0; s2 < 19; s2++) {
-          const uint32_t l = (uint32_t)(clp >> (3 * s2)) & 7u;
-          uint32_t r = 0;
-#pragma unroll
-          for (int t2 = 0; t2 < 19; t2++) {
-            const uint32_t lt2 = (uint32_t)(clp >> (3 * t2)) & 7u;
-            r += (lt2 != 0 && (lt2 < l || (lt2 == l && t2 < s2))) ? 1u : 0u;
-          }
-          if (l) {
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-              if (r / 6 == (uint32_t)q) srt[q] |= (uint32_t)s2 << (5 * (r % 6));
-          }
-          rank += l ? 1u : 0u;
+        for (int t2 = 0; t2 < 19; t2++) {
+          const uint32_t lt2 = (uint32_t)(clp >> (3 * t2)) & 7u;
+          r += (lt2 != 0 && (lt2 < lsym || (lt2 == lsym && t2 < lane))) ? 1u : 0u;
         }
-        (void)rank;
+        // the fields are disjoint: the sum over the lanes is their OR
+        const uint32_t field = lsym ? (uint32_t)lane << (5 * (r % 6)) : 0u;
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+          srt[q] = uni((uint32_t)__shfl((int)wave_incl_scan(r / 6 == (uint32_t)q ? field : 0u), 63));
       }
       __syncthreads();
       WMARK(10);
