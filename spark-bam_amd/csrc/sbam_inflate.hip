@@ -1251,6 +1251,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
     WMARK(0);
     WADD(9, 1);
     if (!wave_build<true>(L, 288, hdist, kDistSubOff, kDistSub)) { ok = false; break; }
+    WMARK(5);  // (the distance table; slot 1: the literal/length table)
     if (!wave_build<false>(L, 0, hlit, kLitSubOff, kLitSub)) { ok = false; break; }
     WMARK(1);
 

@@ -25,7 +25,7 @@ fn(buf, 1)
 f.reset(); f.run(contig_lengths=s.contig_lengths)
 fn(buf, 1)
 v = list(buf)
-names = ["header", "build", "stage", "phaseA", "phaseB", "scanC", "rounds", "b_iters", "total", "headers",
+names = ["header", "build", "stage", "phaseA", "phaseB", "build_dist", "rounds", "b_iters", "total", "headers",
          "hdr_cl_setup", "hdr_chain", "hdr_stage", "warmup"]
 tot = v[8]
 out = {n: v[i] for i, n in enumerate(names)}
@@ -40,7 +40,7 @@ out["tokens"] = tok
 out["phaseC_cycles_per_round"] = {n: round(v[i] / max(v[6], 1)) for i, n in ((24, "prefix_scan"), (25, "run1"), (26, "dumpA"), (27, "dumpR"), (28, "tail"))}
 out["b_iters_per_round"] = round(v[7] / max(v[6], 1), 3)
 out["rounds_per_block"] = round(v[6] / out["blocks"], 3)
-out["cycles_per_header"] = {n: round(v[i] / max(v[9], 1)) for i, n in ((0, "rest"), (10, "cl_setup"), (11, "chain"), (12, "stage"), (1, "build"))}
+out["cycles_per_header"] = {n: round(v[i] / max(v[9], 1)) for i, n in ((0, "rest"), (10, "cl_setup"), (11, "chain"), (12, "stage"), (5, "build_dist"), (1, "build_lit"))}
 out["cycles_per_round"] = {n: round(v[i] / max(v[6], 1)) for i, n in list(enumerate(names[2:6], 2)) + [(13, "warmup")]}
 rsteps = max(v[38], 1)
 rnames = ["positions_zero", "literals", "output_stores", "match_setup", "rounds", "token_wait"]
