@@ -1158,17 +1158,12 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         for (int q = 0; q < 4; q++)
           srt[q] = uni((uint32_t)__shfl((int)wave_incl_scan(r / 6 == (uint32_t)q ? field : 0u), 63));
       }
-      __syncthreads();
-      WMARK(10);
-      const int total = uni(hlit + hdist);  // (uni: the compiler kept it, and the loop below, in VGPRs)
-      int n = 0, p = h.pos;
-      uint32_t prev = 0;
-      while (n < total) {
-        // lane j: the symbol at p + j
-        const int q = p + lane - wq, w = q >> 5, sh = q & 31;
-        const uint64_t x64 = ((uint64_t)L.win[w] | ((uint64_t)L.win[w + 1] << 32)) >> sh;
-        const uint32_t bits = (uint32_t)x64;
-        const uint32_t rev = __builtin_bitreverse32(bits & 127u) >> 25;
+      // the code-length code as a 128-entry table of the next 7 stream bits (in the sorted-symbol scratch, free until
+      // the table builds): length | extra bits << 3 | repeat base << 6 | value << 10 | "previous" << 14 — a window's
+      // 64 decodes are one LDS read each instead of the canonical search
+      uint16_t *cllut = L.sorted();
+      for (int v = lane; v < 128; v += 64) {
+        const uint32_t rev = __builtin_bitreverse32((uint32_t)v) >> 25;
         uint32_t l = 1;
 #pragma unroll
         for (int ll = 1; ll < 7; ll++) l += rev >= lim7[ll] ? 1u : 0u;
@@ -1180,10 +1175,25 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
         const uint32_t sw = dq == 0 ? srt[0] : dq == 1 ? srt[1] : dq == 2 ? srt[2] : srt[3];
         const uint32_t sym = (sw >> (5 * dr)) & 31u;
         const uint32_t xb = sym == 16 ? 2u : sym == 17 ? 3u : sym == 18 ? 7u : 0u;
-        const uint32_t xv = (bits >> l) & ((1u << xb) - 1u);
-        const uint32_t rep = sym < 16 ? 1u : sym == 18 ? 11u + xv : 3u + xv;
+        const uint32_t rb = sym < 16 ? 1u : sym == 18 ? 11u : 3u;
+        cllut[v] = (uint16_t)(l | (xb << 3) | (rb << 6) | ((sym < 16 ? sym : 0u) << 10) | ((sym == 16 ? 1u : 0u) << 14));
+      }
+      __syncthreads();
+      WMARK(10);
+      const int total = uni(hlit + hdist);  // (uni: the compiler kept it, and the loop below, in VGPRs)
+      int n = 0, p = h.pos;
+      uint32_t prev = 0;
+      while (n < total) {
+        // lane j: the symbol at p + j
+        const int q = p + lane - wq, w = q >> 5, sh = q & 31;
+        const uint64_t x64 = ((uint64_t)L.win[w] | ((uint64_t)L.win[w + 1] << 32)) >> sh;
+        const uint32_t bits = (uint32_t)x64;
+        const uint32_t e = cllut[bits & 127u];
+        const uint32_t l = e & 7u, xb = (e >> 3) & 7u;
+        const uint32_t xv = __builtin_amdgcn_ubfe(bits, l, xb);
+        const uint32_t rep = ((e >> 6) & 15u) + xv;
         // packed: advance (5 bits) | repeat (8) | value (4) | value is "previous" (1)
-        const uint32_t info = (l + xb) | (rep << 5) | ((sym < 16 ? sym : 0u) << 13) | ((sym == 16 ? 1u : 0u) << 17);
+        const uint32_t info = (l + xb) | (rep << 5) | (((e >> 10) & 31u) << 13);
         // the true chain through the 64 decoded offsets: only the offsets and the running count are serial
         // (scalar readlanes); values, repeat targets and LDS writes follow for all members at once.  info2 = the
         // info of the symbol after this lane's (a shuffle), so one walk step takes two symbols: two independent
