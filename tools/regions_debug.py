@@ -2,8 +2,9 @@
 """Check k_inflate_regions' hand-over records against a Python restatement of RFC 1951 (regions
 pass): for every BGZF block of a synthetic BAM, its first DEFLATE block's end bit, token count (symbols less the
 end-of-block code) and output bytes; reports the pieced blocks whose record differs and the blocks that went from
-a successful regions pass to the exact decoder (with their DEFLATE block structure).  Needs the GPU build
-(sbam_debug_inflate_resume).   regions_debug.py [--size-mb 20] [--tile-mb 8]"""
+a successful regions pass to the exact decoder (with their DEFLATE block structure).  Needs the regions build of
+branch `exp/regions` (it exports sbam_debug_inflate_resume; the main library does not).
+    regions_debug.py [--size-mb 20] [--tile-mb 8]"""
 import argparse
 import ctypes
 import json
