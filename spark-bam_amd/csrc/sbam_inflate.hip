@@ -1892,6 +1892,9 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
 #endif
           const int n = min(min(Le - done, 16), deff);
           const int src = mO + done - deff;
+          // the keep-mask of the first n bytes, read before the source (it was read after, a second LDS round trip
+          // on every iteration's dependent chain)
+          const uint4 km = *reinterpret_cast<const uint4 *>(s_keep + 4 * n);
           uint32_t v0, v1, v2, v3;
           if (far) {  // below the flushed mark: unaligned 16-B loads, past this CU's L1 (nt)
             // each path waits for its own source here (the prefetched ones: vmcnt(2), the next step's two token
@@ -1916,7 +1919,6 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
             v3 = __builtin_amdgcn_alignbyte(s4, s3, ss);
           }
           // keep the first n bytes
-          const uint4 km = *reinterpret_cast<const uint4 *>(s_keep + 4 * n);
           v0 &= km.x;
           v1 &= km.y;
           v2 &= km.z;
