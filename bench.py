@@ -114,14 +114,54 @@ def copy_peak(dev) -> dict:
                    f"best of grids 2048/8192/32768 x 256 and plain/nontemporal: {best[0]}"}
 
 
-def cpu_baseline(sample_mb: float, threads: int, split_size: int, seed: int, tiles: int = 1):
-    """Oracle (C restatement of the reference algorithm) on a bounded sample of the same synthetic stream:
+REAL_BAM = os.path.join(ROOT, "tests", "fixtures", "5k.bam")  # the reference's test_bams/src/main/resources/5k.bam
+
+
+def make_file(args, target_bytes: int, threads: int, tile_mb: float = None):
+    """The bench input: the synthetic generator (tools/synth_bam.c at zlib level --level), or with --real a real
+    BAM's data blocks tiled to the target size behind its header block (synth.TiledBam)."""
+    import synth
+    if args.real:
+        return synth.TiledBam(args.real, target_bytes)
+    return synth.SynthBam.for_size(target_bytes, tile_mb=args.tile_mb if tile_mb is None else tile_mb, seed=args.seed,
+                                   threads=threads, read_len=args.read_len, level=args.level,
+                                   distinct=args.tiles > 1, cycle=max(args.tiles, 1))
+
+
+def data_desc(args, s) -> str:
+    if args.real:
+        return (f"real: the data blocks of {os.path.relpath(args.real, ROOT)} (the reference's test BAM, htsjdk-written) "
+                f"tiled {s.copies} times behind its header block")
+    return "synthetic (tools/synth_bam.c: %s, zlib-%d BGZF, seed %#x, %s)" % (
+        "150bp paired Illumina-like" if args.read_len == 150 else "long-read 10-50 kb" if args.read_len == 0
+        else f"{args.read_len} bp", args.level, args.seed,
+        f"a cycle of {min(args.tiles, s.copies)} distinct {args.tile_mb:g} MB tiles" if args.tiles > 1
+        else f"one {args.tile_mb:g} MB tile repeated")
+
+
+def pinned_digest(args, s):
+    """The CPU oracle's digests of this exact file and split size (tests/golden/bench_digests.json, written by
+    tests/golden/make_bench_digests.py at full size), or None when this workload was not pinned."""
+    if args.real or args.level != 6 or args.contigs or args.workload != "full-check":
+        return None
+    key = {"file_bytes": int(s.size), "seed": args.seed, "tile_mb": args.tile_mb, "tiles": args.tiles,
+           "read_len": args.read_len, "level": 6, "split_mb": args.split_mb, "reads_to_check": 10}
+    try:
+        db = json.load(open(os.path.join(ROOT, "tests", "golden", "bench_digests.json")))
+    except (OSError, ValueError):
+        return None
+    for e in db:
+        if e["workload"] == key:
+            return e
+    return None
+
+
+def cpu_baseline(args, sample_mb: float, threads: int, split_size: int):
+    """Oracle (C restatement of the reference algorithm) on a bounded sample of the same input stream:
     zlib inflate + full checker at every position + compute-splits, `threads` host threads."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    import synth
-    s = synth.SynthBam.for_size(int(sample_mb * 1e6), tile_mb=min(64.0, sample_mb), seed=seed, threads=threads,
-                                distinct=tiles > 1, cycle=max(tiles, 1))
+    s = make_file(args, int(sample_mb * 1e6), threads, tile_mb=min(64.0, sample_mb))
     data = s.bytes()
     t0 = time.perf_counter()
     f = oracle.BamFile(data, threads=threads)
@@ -135,15 +175,13 @@ def cpu_baseline(sample_mb: float, threads: int, split_size: int, seed: int, til
                       f"compute-splits @ {split_size >> 20} MiB, {wall:.2f} s wall"}
 
 
-def cpu_baseline_load_reads(sample_mb: float, threads: int, split_size: int, seed: int, tiles: int = 1):
+def cpu_baseline_load_reads(args, sample_mb: float, threads: int, split_size: int):
     """Oracle on a bounded sample for the loadReads workload (configs[3]): zlib inflate (`threads` host threads)
     then, per Hadoop split, FindBlockStart → FindRecordStart → the record chain (CanLoadBam.scala:281-334).  The
     oracle stops at record offsets (no field decode into columns), so the CPU side does less work than the GPU."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    import synth
-    s = synth.SynthBam.for_size(int(sample_mb * 1e6), tile_mb=min(64.0, sample_mb), seed=seed, threads=threads,
-                                distinct=tiles > 1, cycle=max(tiles, 1))
+    s = make_file(args, int(sample_mb * 1e6), threads, tile_mb=min(64.0, sample_mb))
     data = s.bytes()
     t0 = time.perf_counter()
     f = oracle.BamFile(data, threads=threads)
@@ -183,6 +221,11 @@ def main():
                          "(two contexts: window w+1's host staging and PCIe copy overlap window w's kernels; "
                          "both inside the timed step)")
     ap.add_argument("--read-len", type=int, default=150, help="0 = long-read config (configs[4])")
+    ap.add_argument("--level", type=int, default=6, help="zlib level of the synthetic BGZF blocks (0 = stored blocks, "
+                                                         "as bgzip -l 0 / samtools view -u write)")
+    ap.add_argument("--real", nargs="?", const=REAL_BAM, default=None,
+                    help="tile a real BAM's data blocks to --size-gb behind its header block (default: the reference's "
+                         "5k.bam) instead of the synthetic generator")
     ap.add_argument("--contigs", type=int, default=0,
                     help="check against N contig lengths (the file's 84, then N - 84 more: a scaffold-level reference, "
                          "so refIdx values up to N - 1 are in range); 0 = the file's own")
@@ -216,14 +259,11 @@ def main():
     cdev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # collective tensors
 
     import sbam
-    import synth
     from sbam import dist as sdist
 
     split_size = int(args.split_mb * (1 << 20))
     t = time.time()
-    s = synth.SynthBam.for_size(int(args.size_gb * 1e9 * world), tile_mb=args.tile_mb, seed=args.seed,
-                                threads=threads, read_len=args.read_len, distinct=args.tiles > 1,
-                                cycle=max(args.tiles, 1))
+    s = make_file(args, int(args.size_gb * 1e9 * world), threads)
     setup_s = time.time() - t
     if args.contigs > len(s.contig_lengths):  # many-contig reference: lengths past the 84 real ones
         extra = np.random.default_rng(args.seed).integers(1000, 1 << 28, args.contigs - len(s.contig_lengths))
@@ -355,6 +395,13 @@ def main():
                                for p in parts]).astype(np.int64)
         parity["digest"] = {"counts": hashlib.sha1(parts[0].counts.astype(np.int64).tobytes()).hexdigest()[:16],
                             "splits": hashlib.sha1(rows.tobytes()).hexdigest()[:16], "n_splits": int(rows.size // 4)}
+        # full-size exactness: the CPU oracle's digests of this same file (tests/golden/make_bench_digests.py)
+        pin = pinned_digest(args, s)
+        parity["digest_pinned"] = pin is not None
+        if pin is not None:
+            parity["digest_oracle"] = pin["digest"]
+            parity["digest_source"] = "tests/golden/bench_digests.json: " + pin["made_by"]
+            parity["ok"] = bool(parity["ok"] and parity["digest"] == pin["digest"])
     if not parity["ok"]:
         log(f"[rank {rank}] PARITY PROPERTY FAILED: {parity}")
 
@@ -404,7 +451,8 @@ def main():
                  "how": "the same step with SBAM_FORCE_PROOF=1: k_chain_proof reads every record's hop although the "
                         "list pass found no missing link (what a shard with one false-positive PASS0 site costs)"}
     achieved = alg[dom] / (avg[dom] * 1e-3) / 1e9 if avg[dom] > 0 else 0.0
-    traffic = measured_traffic(names[dom], args) if (args.read_len == 150 and W == 1) else None
+    traffic = (measured_traffic(names[dom], args) if (args.read_len == 150 and W == 1 and args.level == 6 and
+                                                      not args.real) else None)
 
     # --- pinned host → results (SURVEY §8(d) "with H2D"): the same step with the shard's compressed bytes in
     # pinned host memory, streamed in `e2e_windows` windows through two contexts (window w+1's copy overlaps
@@ -448,7 +496,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline and args.read_len == 150:
             try:
                 base_fn = cpu_baseline if args.workload == "full-check" else cpu_baseline_load_reads
-                cpu = base_fn(args.cpu_sample_mb, threads, split_size, args.seed, args.tiles)
+                cpu = base_fn(args, args.cpu_sample_mb, threads, split_size)
                 cpu["host_nproc"] = nproc
             except Exception as e:  # reported, never substituted for the GPU number
                 log(f"cpu baseline failed: {e!r}")
@@ -472,14 +520,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (tools/synth_bam.c: %s, zlib-6 BGZF, seed %#x, %s)" % (
-                "150bp paired Illumina-like" if args.read_len == 150 else "long-read 10-50 kb" if args.read_len == 0
-                else f"{args.read_len} bp", args.seed,
-                f"a cycle of {min(args.tiles, s.copies)} distinct {args.tile_mb:g} MB tiles" if args.tiles > 1
-                else f"one {args.tile_mb:g} MB tile repeated"),
-            "config": {"workload": ("Synthetic %.0f GB %s BAM per GPU: " % (
-                                   args.size_gb, "Illumina-like" if args.read_len == 150 else
-                                   "long-read" if args.read_len == 0 else f"{args.read_len} bp")) +
+            "data": data_desc(args, s),
+            "config": {"workload": ("%s %.0f GB %s BAM per GPU: " % (
+                                   "Real-data" if args.real else "Synthetic", args.size_gb,
+                                   "5k.bam-tiled" if args.real else
+                                   ("Illumina-like" if args.read_len == 150 else "long-read" if args.read_len == 0
+                                    else f"{args.read_len} bp") + ("" if args.level == 6 else f" zlib-{args.level}"))) +
                                    ("compute-splits @ %g MiB + full-check of every uncompressed offset" % args.split_mb
                                     if fc else "loadReads @ %g MiB splits: records decoded into device columns"
                                     % args.split_mb),

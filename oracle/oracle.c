@@ -222,12 +222,14 @@ static inline uint32_t ref_err(int32_t ri, int32_t rp, const int64_t *lens, int3
 /* full.Checker.apply + build (check/.../check/full/Checker.scala:22-184) at uncompressed offset p of
  * the stream u[0..L).  Java int32 arithmetic (wrap, '/' toward zero) where the Scala uses Int;
  * offsets are int64 (nextOffset is a Long, :53). */
-uint32_t or_check_full(const uint8_t *u, int64_t L, const int64_t *lens, int32_t nref, int64_t p, int32_t R) {
+static inline uint32_t check_full_core(const uint8_t *u, int64_t L, const int64_t *lens, int32_t nref, int64_t p,
+                                       int32_t R, int *hit) {
   int64_t s = p, a = p;
   int32_t k = 0;
   for (;;) {
     if (k == R) return W_SUCCESS | W_K(k); /* :27-28 */
     if (a + 36 > L) {                     /* readFully(buf) fails (:31-48) */
+      *hit = 1;
       if (k > 0 && s == L) return W_SUCCESS | W_K(k);
       return (1u << F_TOO_FEW_FIXED) | W_K(k);
     }
@@ -249,6 +251,7 @@ uint32_t or_check_full(const uint8_t *u, int64_t L, const int64_t *lens, int32_t
       F |= 1u << F_EMPTY_NAME;
     } else {
       if (c + lrn > L) { /* readFully(readNameBuffer) EOF → TooFewBytesForReadName, cigar unevaluated (:140-144) */
+        *hit = 1;
         F |= 1u << F_FEW_NAME;
         return F | W_K(k);
       }
@@ -266,6 +269,7 @@ uint32_t or_check_full(const uint8_t *u, int64_t L, const int64_t *lens, int32_t
     int cig_err = 0; /* :111-136 */
     for (int32_t i = 0; i < nc; i++) {
       if (c + 4 > L) {
+        *hit = 1;
         F |= 1u << F_FEW_CIGAR;
         cig_err = 1;
         break;
@@ -286,6 +290,7 @@ uint32_t or_check_full(const uint8_t *u, int64_t L, const int64_t *lens, int32_t
     }
     if (F) return F | W_K(k);
     int64_t nxt = s + 4 + (int64_t)bs; /* :53, :167-172 */
+    if (nxt > L) *hit = 1;
     if (nxt > c)
       a = nxt > L ? L : nxt; /* skip past EOF: parity unpinned; clamp */
     else
@@ -293,6 +298,11 @@ uint32_t or_check_full(const uint8_t *u, int64_t L, const int64_t *lens, int32_t
     s = nxt;
     k++;
   }
+}
+
+uint32_t or_check_full(const uint8_t *u, int64_t L, const int64_t *lens, int32_t nref, int64_t p, int32_t R) {
+  int hit = 0;
+  return check_full_core(u, L, lens, nref, p, R, &hit);
 }
 
 /* eager.Checker.apply (check/.../check/eager/Checker.scala:24-126): same checks, boolean result;
@@ -359,4 +369,61 @@ int64_t or_record_chain(const uint8_t *u, int64_t L, int64_t x0, int64_t x_end, 
     x = x + 4 + (int64_t)bs;
   }
   return n;
+}
+
+/* ------------------------------------------------------------------------------------------------
+ * Windowed forms for oracle runs over files larger than memory (tools/pin_bench_digests.py).  The
+ * stream is held as a window u[0..L) that is a prefix of the rest of the file: a position's result
+ * equals the whole file's unless its evaluation reached the window's end (one of the `> L` tests
+ * above fired), which these functions count in *hits so that the caller can widen the window.
+ * ---------------------------------------------------------------------------------------------- */
+
+/* or_counts_range + the close-call pair histogram of key-2 results (FullCheck.scala:141-191: the
+ * first two flags, or (flag, flag) when the second non-zero field is readsBeforeError) and the
+ * TooFewFixedBlockBytes-only results dropped from the Counts.  scal = {n_success, n_too_few_fixed, hits}. */
+void or_counts_window(const uint8_t *u, int64_t L, const int64_t *lens, int32_t nref, int64_t p0, int64_t p1,
+                      int32_t R, int64_t *counts, int64_t *npos, int64_t *rbe, int64_t *pair, int64_t *scal) {
+  for (int64_t p = p0; p < p1; p++) {
+    int hit = 0;
+    uint32_t w = check_full_core(u, L, lens, nref, p, R, &hit);
+    scal[2] += hit;
+    if (w & W_SUCCESS) {
+      scal[0]++;
+      continue;
+    }
+    uint32_t F = w & 0x7ffff;
+    uint32_t k = (w >> 24) & 0x7f;
+    if (F == 1u && k == 0) {
+      scal[1]++;
+      continue;
+    }
+    int key = __builtin_popcount(F) + (k > 0);
+    npos[key]++;
+    for (int f = 0; f < 19; f++)
+      if (F & (1u << f)) counts[key * 19 + f]++;
+    if (k > 0) rbe[key * 128 + k]++;
+    if (key == 2) {
+      int f0 = __builtin_ctz(F);
+      uint32_t rest = F & (F - 1);
+      int f1 = rest ? __builtin_ctz(rest) : f0;
+      pair[f0 * 19 + f1]++;
+    }
+  }
+}
+
+/* or_find_record_start with the window-end test counted in *hits. */
+int64_t or_find_record_start_window(const uint8_t *u, int64_t L, const int64_t *lens, int32_t nref, int64_t x0,
+                                    int32_t R, int64_t max_read_size, int64_t *hits) {
+  for (int64_t i = 0; i < max_read_size; i++) {
+    int64_t x = x0 + i;
+    if (x >= L) {
+      (*hits)++;
+      return -1;
+    }
+    int hit = 0;
+    uint32_t w = check_full_core(u, L, lens, nref, x, R, &hit);
+    *hits += hit;
+    if (w & W_SUCCESS) return x;
+  }
+  return -1;
 }

@@ -79,7 +79,7 @@ struct sbam_ctx {
   size_t tokbase_cap = 0;
   int32_t *d_slow = nullptr;  // blocks the wave decoder hands to the exact per-lane decoder
   size_t slow_cap = 0;
-  unsigned int *d_icnt = nullptr;  // slow-path blocks, slow-path work, resolve work
+  unsigned int *d_icnt = nullptr;  // slow-path blocks, slow-path work, resolve work, stored-only blocks
   int64_t inflate_slow = -1;       // blocks the last sbam_inflate decoded on the exact per-lane path
   // split chains: per-split first record / chain end / count / record base (grow-only)
   int64_t *d_sx = nullptr, *d_se = nullptr, *d_sn = nullptr, *d_sb = nullptr;
@@ -361,8 +361,8 @@ int sbam_reserve(sbam_ctx *c, int64_t comp_bytes, int64_t n_blocks, int64_t ubyt
   // stage drops its stages (sbam_reset) when one grows: a later query re-runs them instead of reading uninitialised
   // device memory.  The resident compressed bytes and the contig lengths are kept.
   bool grew = false;
-  auto grow = [&](auto **p, size_t *cap, size_t n) {
-    grew |= *cap < std::max<size_t>(n, 1);
+  auto grow = [&](auto **p, size_t *cap, size_t n) {  // (a buffer never allocated held no stage's data)
+    grew |= *p != nullptr && *cap < std::max<size_t>(n, 1);
     return ensure(p, cap, n);
   };
   if ((size_t)comp_bytes + kCompPad > c->comp_cap) {  // keep the resident bytes (sbam_load replaces them anyway)
@@ -393,8 +393,8 @@ int sbam_reserve(sbam_ctx *c, int64_t comp_bytes, int64_t n_blocks, int64_t ubyt
     c->arena_cap -= 1024;
   }
   HIPCHK(c, grow(&c->d_tokbase, &c->tokbase_cap, n_blocks));
-  HIPCHK(c, grow(&c->d_slow, &c->slow_cap, n_blocks));
-  grew |= (size_t)((ubytes + 63) / 64) + 1 > c->bitmap_cap;
+  HIPCHK(c, grow(&c->d_slow, &c->slow_cap, 2 * n_blocks));  // (the exact decoder's list, then the stored-only list)
+  grew |= c->d_bitmap != nullptr && (size_t)((ubytes + 63) / 64) + 1 > c->bitmap_cap;
   if (int rc = ensure_bitmap(c, 0, ubytes)) return rc;
   HIPCHK(c, grow(&c->d_tcnt, &c->tcnt_cap, (size_t)(4 * check_tiles(0, ubytes) + 8)));  // (x0 may add a tile)
   if (n_records > 0) {  // the chain pass's PASS0 list (about one entry per record) and loadReads' offsets
@@ -620,7 +620,7 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
     c->arena_cap -= 1024;
   }
   HIPCHK(c, ensure(&c->d_tokbase, &c->tokbase_cap, nb));
-  HIPCHK(c, ensure(&c->d_slow, &c->slow_cap, nb));
+  HIPCHK(c, ensure(&c->d_slow, &c->slow_cap, 2 * nb));  // (the exact decoder's list, then the stored-only list)
   if (!c->d_icnt) HIPCHK(c, dalloc(&c->d_icnt, 4));
   unsigned long long *d_used = reinterpret_cast<unsigned long long *>(c->d_small + 16);
   unsigned long long ferr = 0;
@@ -633,7 +633,7 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
       Timer t(c, "inflate");
       {
         Timer t1(c, "inflate_decode");
-        HIPCHK(c, launch_inflate_decode(c->d_comp, c->D, bt, tp, d_status, d_found, c->d_slow, c->d_icnt, c->stream));
+        HIPCHK(c, launch_inflate_decode(c->d_comp, c->D, bt, tp, c->d_u, d_status, d_found, c->d_slow, c->d_icnt, c->stream));
       }
       Timer t2(c, "inflate_resolve");
       // (the slow list is consumed by now: the resolver's redo list reuses d_slow, its count is d_icnt[2])

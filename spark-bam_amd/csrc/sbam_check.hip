@@ -1406,6 +1406,12 @@ constexpr int kEwQ = 128;                // survivor queue per wave (a tile's su
 constexpr int kEwWaves = 4;
 constexpr int kEwHalo = 64;              // bytes past the tile in the window (>= 32: nextRefIdx of the last positions)
 constexpr int kEwWin = kTile + kEwHalo;  // per-wave LDS window
+// The wave's layout assumes these: a tile is 8 pieces x 64 lanes x 16 B (piece k, lane l at 1024 k + 16 l; the queue
+// holds tile offsets as uint16), the halo is whole 16-B pieces loaded by lanes 0 .. kEwHalo / 16 - 1 (piece 512), and
+// the tile's bitmap leaves as one 16-B store per lane.
+static_assert(kTile == 8 * 64 * 16, "k_eager_wave: a tile is 8 pieces of 64 lanes x 16 B");
+static_assert(kEwHalo >= 32 && kEwHalo % 16 == 0 && kEwHalo <= 64 * 16, "k_eager_wave: halo of whole 16-B pieces");
+static_assert(kTile / 32 == 64 * 4, "k_eager_wave: the tile's bitmap is one u32x4 per lane");
 // eager.Checker record-0 checks at position rel of a wave's window (win = the tile's bytes from base), given the
 // fixed fields f[]: check_first<true, true>'s pass/fail, straight from the bytes (no op-class / name-character
 // bitmaps: survivors are few, and a true record's name and CIGAR are short).

@@ -1065,6 +1065,88 @@ extern "C" int sbam_debug_wave_stats(unsigned long long *out, int reset) {
 #define RMARK(k) do {} while (0)
 #endif
 
+// ---- stored blocks (BTYPE 00) -----------------------------------------------------------------------------------
+// zlib level 0 (bgzip -l 0, samtools view -u) and incompressible input at any level make stored DEFLATE blocks: LEN
+// raw bytes behind a byte-aligned LEN / NLEN pair (RFC 1951 3.2.4).  A BGZF payload whose DEFLATE stream is only
+// stored blocks is a copy: the wave walks the block headers (wave-uniform, one or a few per payload), then copies the
+// bytes straight to the output (unaligned 16-B loads, 16-B aligned stores; byte stores for the partial 16-B chunks at
+// a stored block's edges — a BGZF block's first and last chunks are shared with its neighbours) and marks the block
+// done for the resolver (TokPool::base = kTokDone): no tokens, no resolve.  Anything else — a stored block after
+// Huffman output, LEN != ~NLEN, data past the payload, a total other than ISIZE, more than kMaxStored blocks — goes to
+// the exact decoder as before, which has zlib's semantics for every case (Stream.scala:49-54).  (Round 5 sent every
+// stored block there: one lane emitting 2 literal tokens per step into the arena, then the resolver.)
+constexpr int kMaxStored = 64;
+constexpr int64_t kTokDone = -2;  // TokPool::base of a block already written to the output
+
+// bitp: payload-relative bit position of the first stored block's header (BFINAL, BTYPE 00).  seg: 2 * kMaxStored
+// dwords of LDS.  Returns false (nothing written) when the payload is not a clean chain of stored blocks producing
+// exactly ISIZE bytes.
+SB_DEV bool stored_copy(const uint8_t *__restrict__ d, int64_t a, int dlen, int bitp, int32_t us,
+                        uint8_t *__restrict__ ob, int64_t U0, uint32_t *seg) {
+  const int lane = (int)threadIdx.x;
+  int n = 0, o = 0;
+  if ((bitp + 3 + 7) / 8 > dlen) return false;
+  bool fin;
+  {
+    const uint32_t h3 = (uint32_t)d[a + (bitp >> 3)] | (uint32_t)d[a + (bitp >> 3) + 1] << 8;
+    const uint32_t hb = (h3 >> (bitp & 7)) & 7u;
+    if (((hb >> 1) & 3u) != 0u) return false;
+    fin = (hb & 1u) != 0u;
+    bitp += 3;
+  }
+  for (;;) {
+    const int byp = (bitp + 7) >> 3;  // LEN / NLEN start on the next byte boundary
+    if (byp + 4 > dlen || n == kMaxStored) return false;
+    const uint32_t len = (uint32_t)d[a + byp] | (uint32_t)d[a + byp + 1] << 8;
+    const uint32_t nlen = (uint32_t)d[a + byp + 2] | (uint32_t)d[a + byp + 3] << 8;
+    if ((len ^ 0xffffu) != nlen) return false;
+    const int dat = byp + 4;
+    if (dat + (int)len > dlen) return false;
+    if (lane == 0) {
+      seg[2 * n] = (uint32_t)o;
+      seg[2 * n + 1] = (uint32_t)dat;
+    }
+    n++;
+    o += (int)len;
+    if (o > us) return false;
+    if (fin) break;
+    const int nb = dat + (int)len;  // the next block's header byte (byte-aligned after a stored block)
+    if (nb >= dlen) return false;
+    const uint32_t h3 = d[a + nb];
+    if (((h3 >> 1) & 3u) != 0u) return false;
+    fin = (h3 & 1u) != 0u;
+    bitp = nb * 8 + 3;
+  }
+  if (o != us) return false;
+  __syncthreads();  // (one wave: the segment list is visible to every lane)
+  for (int j = 0; j < n; j++) {
+    const int o0 = (int)seg[2 * j], o1 = j + 1 < n ? (int)seg[2 * j + 2] : us;
+    const uint8_t *src = d + a + (int)seg[2 * j + 1] - o0;  // output byte x of this stored block is src[x]
+    const int c0 = o0 + (int)((16 - ((U0 + o0) & 15)) & 15), c1 = o1 - (int)((U0 + o1) & 15);
+    if (c0 + 16 <= c1) {
+      // 16-B aligned output chunks [c0, c1): four loads in flight per lane before their stores
+      int x = c0 + 16 * lane;
+      for (; x + 3 * 1024 + 16 <= c1; x += 4 * 1024) {
+        const u32x4 v0 = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src + x));
+        const u32x4 v1 = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src + x + 1024));
+        const u32x4 v2 = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src + x + 2048));
+        const u32x4 v3 = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src + x + 3072));
+        *reinterpret_cast<u32x4 *>(ob + x) = v0;
+        *reinterpret_cast<u32x4 *>(ob + x + 1024) = v1;
+        *reinterpret_cast<u32x4 *>(ob + x + 2048) = v2;
+        *reinterpret_cast<u32x4 *>(ob + x + 3072) = v3;
+      }
+      for (; x + 16 <= c1; x += 1024)
+        *reinterpret_cast<u32x4 *>(ob + x) = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(src + x));
+      if (lane < c0 - o0) ob[o0 + lane] = src[o0 + lane];  // (< 16 bytes each side)
+      if (lane < o1 - c1) ob[c1 + lane] = src[c1 + lane];
+    } else {
+      for (int x = o0 + lane; x < o1; x += 64) ob[x] = src[x];
+    }
+  }
+  return true;
+}
+
 __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restrict__ d, int64_t D, BlockTable bt,
                                                      TokPool tp, int32_t *__restrict__ status,
                                                      int32_t *__restrict__ found, int32_t *__restrict__ slow,
@@ -1094,7 +1176,7 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
   uint8_t *lens = L.lens();
   int pos = skip;
   int out = 0, ntok = 0;
-  bool ok = true;
+  bool ok = true, stored = false;
 #ifdef SBAM_WAVE_STATS
   uint64_t ws_[32] = {0};  // (slots 32.. are the resolver's)
   uint64_t wt_ = __builtin_amdgcn_s_memtime();
@@ -1253,7 +1335,9 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
       h.pos = p;
       __syncthreads();
       if (lens[256] == 0) { ok = false; break; }  // no end-of-block code
-    } else {  // stored (rare in BGZF) or invalid: the slow decoder
+    } else {  // stored from the first output byte: k_inflate_stored's copy; else (a stored block after Huffman output,
+              // an invalid type) the slow decoder
+      stored = type == 0 && out == 0 && ntok == 0;
       ok = false;
       break;
     }
@@ -1677,9 +1761,38 @@ __global__ __launch_bounds__(64, 4) void k_inflate_wave(const uint8_t *__restric
     if (ok) {
       status[b] = INF_OK;
       found[b] = us;
+    } else if (stored) {
+      slow[bt.n + atomicAdd(nslow + 3, 1u)] = (int32_t)b;
     } else {
       slow[atomicAdd(nslow, 1u)] = (int32_t)b;
     }
+  }
+}
+
+// The stored-only blocks k_inflate_wave listed (slow[bt.n ..], count nslow[3]): one wave each, grid-stride over the
+// list.  The copy starts at the payload's first DEFLATE block; a block whose payload is not a clean stored chain from
+// there (e.g. empty Huffman blocks before the stored ones, which no common encoder writes) goes to the exact
+// decoder's list.
+__global__ __launch_bounds__(64) void k_inflate_stored(const uint8_t *__restrict__ d, BlockTable bt, TokPool tp,
+                                                      uint8_t *__restrict__ out, int32_t *__restrict__ status,
+                                                      int32_t *__restrict__ found, int32_t *__restrict__ slow,
+                                                      unsigned int *nslow) {
+  __shared__ uint32_t seg[2 * kMaxStored];
+  const unsigned n = nslow[3];
+  for (unsigned i = blockIdx.x; i < n; i += gridDim.x) {
+    const int64_t b = slow[bt.n + i];
+    const int64_t a = bt.start[b] + bt.hsize[b], U0 = bt.uoff[b];
+    const int32_t dlen = bt.csize[b] - bt.hsize[b] - 8, us = bt.usize[b];
+    if (stored_copy(d, a, dlen, 0, us, out + U0, U0, seg)) {
+      if (threadIdx.x == 0) {
+        tp.base[b] = kTokDone;
+        status[b] = INF_OK;
+        found[b] = us;
+      }
+    } else if (threadIdx.x == 0) {
+      slow[atomicAdd(nslow, 1u)] = (int32_t)b;
+    }
+    __syncthreads();  // (seg is reused by the next block)
   }
 }
 
@@ -1767,11 +1880,11 @@ __global__ __launch_bounds__(64) void k_inflate_resolve(BlockTable bt, uint8_t *
   }
   const int64_t b = list ? list[blockIdx.x] : blockIdx.x;
   const int ae = found[b];  // output bytes of the block
-  if (ae <= 0) return;
+  const int64_t tbase = pool.base[b];
+  if (ae <= 0 || tbase == kTokDone) return;  // (kTokDone: the decoder copied a stored-only block itself)
   const int64_t U0 = bt.uoff[b];
   uint8_t *ob = out + U0;
   const uint32_t Gr = (uint32_t)U0 & G::kMask;  // ring byte of position 0
-  const int64_t tbase = pool.base[b];
   const uint16_t *tk =
       reinterpret_cast<const uint16_t *>(tbase >= 0 ? pool.arena + tbase : pool.main + tok_region(U0, b));
   const int F0 = (int)((16 - (U0 & 15)) & 15);  // first position on a 16-B boundary
@@ -1999,12 +2112,16 @@ hipError_t launch_first_error(const int32_t *status, int64_t n, unsigned long lo
 }
 
 
-hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, TokPool tok, int32_t *status,
-                                 int32_t *found, int32_t *slow, unsigned int *counters, hipStream_t s) {
-  // counters: [0] slow-path blocks, [1] slow-path work (zeroed first: the host reads [0] back even for 0 blocks)
-  (void)hipMemsetAsync(counters, 0, 3 * sizeof(unsigned int), s);
+hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, TokPool tok, uint8_t *out,
+                                 int32_t *status, int32_t *found, int32_t *slow, unsigned int *counters,
+                                 hipStream_t s) {
+  // counters: [0] slow-path blocks, [1] slow-path work, [3] stored-only blocks (zeroed first: the host reads [0] back
+  // even for 0 blocks).  slow: 2 x bt.n entries, the exact decoder's list from 0, the stored-only list from bt.n.
+  (void)hipMemsetAsync(counters, 0, 4 * sizeof(unsigned int), s);
   if (bt.n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_inflate_wave, dim3((unsigned)bt.n), dim3(64), 0, s, d, D, bt, tok, status, found, slow,
+                     counters + 0);
+  hipLaunchKernelGGL(k_inflate_stored, dim3(4096), dim3(64), 0, s, d, bt, tok, out, status, found, slow,
                      counters + 0);
   hipLaunchKernelGGL(k_inflate_slow, dim3(256), dim3(kDecThreads), 0, s, d, D, bt, tok, slow, counters + 0, status,
                      found, counters + 1);

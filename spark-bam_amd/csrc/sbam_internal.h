@@ -104,8 +104,9 @@ inline size_t inflate_arena_bytes(int64_t L) {
   if (e && *e) return (size_t)std::atoll(e) << 20;
   return (size_t)L / 16 + (1u << 20);
 }
-hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, TokPool tok, int32_t *status,
-                                 int32_t *found, int32_t *slow, unsigned int *counters, hipStream_t s);
+hipError_t launch_inflate_decode(const uint8_t *d, int64_t D, BlockTable bt, TokPool tok, uint8_t *out,
+                                 int32_t *status, int32_t *found, int32_t *slow, unsigned int *counters,
+                                 hipStream_t s);
 // list (nlist blocks) or every block; blocks with a distance past their first byte are appended to redo[*nredo]
 hipError_t launch_inflate_resolve(BlockTable bt, uint8_t *out, TokPool tok, const int32_t *found,
                                   const int32_t *list, int64_t nlist, int32_t *redo, unsigned int *nredo,

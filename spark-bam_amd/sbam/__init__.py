@@ -345,15 +345,14 @@ class BamFile:
 
     def reserve(self, comp_bytes: int, n_blocks: int, ubytes: int, n_records: int = 0):
         """sbam_reserve: size the device buffers for windows up to these sizes, so no later load reallocates.  A
-        buffer that grows drops the context's stages (their device data is gone); the scan and inflate this object
-        had run are then run again from the resident bytes."""
-        had_scan, had_stream = self.n_blocks is not None, self.uncompressed_size is not None
+        buffer that grows drops the context's stages (their device data is gone); an inflated stream this object
+        had is then inflated again from the resident bytes (a dropped block scan needs nothing here: the library
+        re-runs it on its next use, ensure_blocks)."""
+        had_stream = self.uncompressed_size is not None
         self._check(self.L.sbam_reserve(self.ctx, int(comp_bytes), int(n_blocks), int(ubytes), int(n_records)))
         if had_stream and self.L.sbam_read_uncompressed(self.ctx, 0, 0, None) == ERR_STATE:
             self.n_blocks = self._scan()
             self.inflate()
-        elif had_scan and not had_stream:
-            self.n_blocks = self._scan()
 
     @property
     def loads_to_eof(self) -> bool:

@@ -26,6 +26,11 @@ import numpy as np
 import sbam
 
 
+class NoDataBlock(sbam.SbamError):
+    """The block chain has no block with data at a position: the EOF marker, an empty block (MetadataStream stops
+    there) or a position that is not a block start."""
+
+
 class LazyBlockChecker:
     """eager.Checker (`kind="eager"`: apply → bool, eager/Checker.scala:24-126) or full.Checker (`kind="full"`: apply →
     the sbam.h result word, full/Checker.scala:22-184), computed a window of blocks at a time on first use.
@@ -65,7 +70,7 @@ class LazyBlockChecker:
             f.run(contig_lengths=self.contig_lengths)
             st, cs, us, uo = f.blocks()
             if st.size == 0 or int(st[0]) != block_pos:
-                raise sbam.SbamError(f"no BGZF block starts at {block_pos}")
+                raise NoDataBlock(f"no BGZF block starts at {block_pos}")
             # the blocks of the first half of the window (all of them when it reaches EOF): the second half is the
             # halo their chains read
             end = hi if f.loads_to_eof else lo + (hi - lo) // 2
@@ -104,9 +109,11 @@ class LazyBlockChecker:
         further block with data there: the EOF marker, an empty block or the file's end (MetadataStream stops)."""
         calls = self.cache.get(block_pos)
         if calls is None:
+            if not first and block_pos >= self.file_size:
+                return None
             try:
                 self._fill(block_pos)
-            except sbam.SbamError:
+            except NoDataBlock:  # (only this: a HIP, inflate or halo error on a later window still raises)
                 if first:
                     raise
                 return None

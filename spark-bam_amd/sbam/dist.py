@@ -366,9 +366,13 @@ def deflate_token_count(payload: bytes, limit: int = 1 << 20) -> int:
                 bits(16)
                 tokens += ln
                 out += ln
-                skip = max(0, ln - bc // 8)
-                bb = bc = 0 if skip else bb
-                pos += skip
+                inbuf = bc // 8  # whole bytes already in the bit buffer (bc is a multiple of 8 here)
+                if ln >= inbuf:
+                    bb = bc = 0
+                    pos += ln - inbuf
+                else:
+                    bb >>= 8 * ln
+                    bc -= 8 * ln
             elif typ in (1, 2):
                 if typ == 1:
                     ll = [8] * 144 + [9] * 112 + [7] * 24 + [8] * 8

@@ -1,7 +1,7 @@
 """The eager record-0 pass (k_eager_wave, one wave per interior tile) against the oracle on inputs that stress its
 paths: a tile where every position survives the refIdx / nextRefIdx prefilter (a 45 KB run of zero bytes inside a
-record: more than the wave's 256-entry survivor queue holds, so the queue runs in rounds), survivors at the tile's
-last positions (whose nextRefIdx lies in the 32 B past the tile), and the plain fixtures.  eager.Checker =
+record: more than the wave's 128-entry survivor queue holds, so the queue runs in rounds), survivors at the tile's
+last positions (whose nextRefIdx lies in the 64 B the wave loads past the tile), and the plain fixtures.  eager.Checker =
 eager/Checker.scala:24-126; its calls equal full.Checker's success bit (both are "the first R records pass")."""
 import os
 import struct

@@ -120,24 +120,103 @@ def test_inflate_corrupted_payloads(seed):
     assert gpu_result(data) == oracle_result(data)
 
 
+def stored_chain(p: bytes) -> bool:
+    """Whether a raw DEFLATE stream is only stored blocks from its first bit to a final block (RFC 1951 3.2.4) —
+    the payloads k_inflate_stored copies."""
+    pos = 0  # bit position
+    while True:
+        if (pos >> 3) >= len(p):
+            return False
+        hb = (p[pos >> 3] | (p[(pos >> 3) + 1] << 8 if (pos >> 3) + 1 < len(p) else 0)) >> (pos & 7)
+        if (hb >> 1) & 3:
+            return False
+        byp = (pos + 3 + 7) >> 3
+        if byp + 4 > len(p):
+            return False
+        ln, nln = struct.unpack("<HH", p[byp:byp + 4])
+        if ln ^ 0xffff != nln or byp + 4 + ln > len(p):
+            return False
+        if hb & 1:
+            return True
+        pos = (byp + 4 + ln) * 8
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(4))
 def test_wave_decoder_takes_every_compressed_block(seed):
-    """Only the payloads of stored DEFLATE blocks (level 0, and incompressible data at any level) go to the
-    per-lane fallback; fixed, dynamic, Huffman-only and RLE blocks are decoded by the wave-parallel decoder (whose
-    output test_inflate_shapes_bit_exact checks)."""
+    """Fixed, dynamic, Huffman-only and RLE blocks are decoded by the wave-parallel decoder, and payloads that are only
+    stored blocks (level 0; incompressible data at any level) are copied by k_inflate_stored; only a payload whose
+    first DEFLATE block is stored but which goes on with Huffman blocks takes the per-lane exact decoder (round 6;
+    before, every payload starting with a stored block did).  The bytes: test_inflate_shapes_bit_exact."""
     import sbam
     data = build_file(seed)
-    stored = 0
+    exact = 0
     for i, raw in enumerate(sample_inputs(seed)):
         level, strat = SHAPES[(i + seed) % len(SHAPES)]
-        stored += ((deflate(raw, level, strat)[0] >> 1) & 3) == 0  # first block's BTYPE
+        p = deflate(raw, level, strat)
+        exact += ((p[0] >> 1) & 3) == 0 and not stored_chain(p)  # first block's BTYPE stored, not all stored
     g = sbam.BamFile(data, inflate=False)
     try:
         g.inflate()
-        assert g.inflate_fallbacks() == stored
+        assert g.inflate_fallbacks() == exact
     finally:
         g.close()
+
+
+def stored_block(data: bytes, final: bool) -> bytes:
+    """One byte-aligned stored DEFLATE block (the header's 5 padding bits are zero)."""
+    return bytes([1 if final else 0]) + struct.pack("<HH", len(data), len(data) ^ 0xffff) + data
+
+
+def stored_shape_blocks(seed):
+    """(payload, ISIZE) pairs of stored-block payloads that zlib inflates to exactly ISIZE bytes."""
+    r = np.random.default_rng(seed)
+    blocks = []
+    for n in (1, 15, 16, 17, 1000, 4096, 65480, int(r.integers(2, 65480))):  # (BSIZE is a u16: <= 65510 stored bytes)
+        x = r.integers(0, 256, n, dtype=np.uint8).tobytes()
+        blocks.append((deflate(x, 0), n))
+    x = r.integers(0, 256, 65000, dtype=np.uint8).tobytes()
+    blocks.append((stored_block(x[:40001], False) + stored_block(x[40001:], True), 65000))
+    for _ in range(6):  # chains of small stored blocks, some empty
+        parts = [r.integers(0, 256, int(r.integers(0, 40)), dtype=np.uint8).tobytes()
+                 for _ in range(int(r.integers(2, 60)))]
+        blocks.append((b"".join(stored_block(x, i == len(parts) - 1) for i, x in enumerate(parts)),
+                       sum(len(x) for x in parts)))
+    x = r.integers(0, 256, 3000, dtype=np.uint8).tobytes()
+    blocks.append((b"".join(stored_block(x[i:i + 30], i + 30 >= 3000) for i in range(0, 3000, 30)), 3000))  # 100
+    c = zlib.compressobj(6, zlib.DEFLATED, -15)
+    hx = b"ACGT" * 2000
+    blocks.append((c.compress(hx) + c.flush(zlib.Z_SYNC_FLUSH) + stored_block(x[:777], True), len(hx) + 777))
+    good = stored_block(x[:500], True)
+    blocks.append((good, 500))
+    blocks.append((good + b"\x17\x42", 500))  # trailing bytes after the final block (zlib ignores them)
+    return blocks, good
+
+
+def test_stored_shapes_oracle():
+    blocks, _ = stored_shape_blocks(0)
+    kind, out = oracle_result(b"".join(bgzf_block(p, n) for p, n in blocks) + EOF_BLOCK)
+    assert kind == "ok" and len(out) == sum(n for _, n in blocks)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(3))
+def test_stored_payload_shapes(seed):
+    """Payloads of stored blocks against zlib: level 0 of sizes up to a full BGZF block (one or two stored blocks), chains of
+    many small and zero-length stored blocks (every alignment of a block edge against the output's 16-B chunks), a
+    stored block after a sync-flushed Huffman block (the exact decoder), and the cases the copy must hand to the exact
+    decoder: LEN != ~NLEN, data past the payload, no final block, ISIZE other than the chain's bytes, trailing bytes
+    after the final block, more stored blocks than the copy lists (64)."""
+    blocks, good = stored_shape_blocks(seed)
+    data = b"".join(bgzf_block(p, n) for p, n in blocks) + EOF_BLOCK
+    assert gpu_result(data) == oracle_result(data)
+    bad = [(good[:3] + bytes([good[3] ^ 1]) + good[4:], 500),  # NLEN
+           (good[:-1], 500),                                     # data past the payload
+           (stored_block(good[5:], False), 500),                 # no final block
+           (good, 499), (good, 501), (good, 0)]                  # ISIZE other than the chain's bytes
+    for p, n in bad:
+        data = b"".join(bgzf_block(q, m) for q, m in blocks[:3] + [(p, n)] + blocks[3:5]) + EOF_BLOCK
+        assert gpu_result(data) == oracle_result(data), (p[:8], n)
 
 
 @pytest.mark.gpu
@@ -281,18 +360,25 @@ def test_inflate_round_boundary_distance(distance_ok):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("arena_mb", ["", "256"])
-@pytest.mark.parametrize("kind", ["stored", "huffman_only"])
+@pytest.mark.parametrize("kind", ["stored", "huffman_then_stored", "huffman_only"])
 def test_token_arena_growth(kind, arena_mb, monkeypatch):
-    """Blocks whose tokens outgrow the main token regions (1 B per output byte): stored blocks (the exact decoder,
-    which always writes into the arena) and Huffman-only blocks (1 token = 2 B per byte: the wave decoder moves them
-    into the arena).  32 MiB of them exceed the default arena (1/16 of the output + 1 MiB), so the first inflate
-    overflows and the host grows the arena and inflates again; the bytes equal zlib's either way."""
+    """Blocks whose tokens outgrow the main token regions (1 B per output byte): a stored block after Huffman output
+    (the exact decoder, which always writes into the arena) and Huffman-only blocks (1 token = 2 B per byte: the wave
+    decoder moves them into the arena).  32 MiB of them exceed the default arena (1/16 of the output + 1 MiB), so the
+    first inflate overflows and the host grows the arena and inflates again; the bytes equal zlib's either way.
+    Level-0 payloads (only stored blocks) need no tokens at all since round 6: k_inflate_stored copies them."""
     import sbam
     r = np.random.default_rng(11)
     n, size = 512, 65498
     if kind == "stored":
         datas = [r.integers(0, 256, size, dtype=np.uint8).tobytes() for _ in range(n)]
         pays = [deflate(x, 0) for x in datas]
+    elif kind == "huffman_then_stored":  # a sync-flushed Huffman block, then the rest as one final stored block
+        datas = [b"ACGT" * 64 + r.integers(0, 256, size - 256, dtype=np.uint8).tobytes() for _ in range(n)]
+        pays = []
+        for x in datas:
+            c = zlib.compressobj(6, zlib.DEFLATED, -15)
+            pays.append(c.compress(x[:256]) + c.flush(zlib.Z_SYNC_FLUSH) + stored_block(x[256:], True))
     else:
         datas = [r.integers(0, 16, size, dtype=np.uint8).tobytes() for _ in range(n)]
         pays = [deflate(x, 6, zlib.Z_HUFFMAN_ONLY) for x in datas]
@@ -305,6 +391,6 @@ def test_token_arena_growth(kind, arena_mb, monkeypatch):
     g = sbam.BamFile(data, inflate=False)
     try:
         g.inflate()
-        assert g.inflate_fallbacks() == (n if kind == "stored" else 0)
+        assert g.inflate_fallbacks() == (n if kind == "huffman_then_stored" else 0)
     finally:
         g.close()

@@ -135,3 +135,30 @@ def test_synthetic_1gb_properties():
         assert np.array_equal(sw, se) and np.array_equal(cw["offset"], ce["offset"])
         off, bs = cp["offset"], cp["block_size"].astype(np.int64)
         assert np.array_equal(off[1:], off[:-1] + 4 + bs[:-1])
+
+
+@pytest.mark.parametrize("R", [1, 2, 10])
+@pytest.mark.parametrize("split_kb", [20, 1 << 20])
+def test_last_pass0_hop_inside_range(R, split_kb):
+    """ADVICE r05 (k_p0_links' last list entry): 100 zero bytes after the last record of 2.bam, inside its last data
+    block.  The last true record is then the list's last PASS0 site and its hop lands inside the checked range on a
+    position that is not a PASS0 site (zeros fail record 0: noReadName).  RecordStream walks through the zeros as
+    25 four-byte records (block_size 0), so a loadReads that trusted the eager bitmap there would miss them: the last
+    entry must count as a missing link, the chain proof must run and fail, and the walk must give the oracle's
+    partitions.  Under the round-4 rule (last entry always linked) the proof was skipped for R = 1."""
+    import oracle
+    import sbam
+    from test_eager_wave import bgzf
+    base = oracle.BamFile(open(f"{FIXTURES}/2.bam", "rb").read())
+    blob = bgzf(base.u[:base.L].tobytes() + b"\x00" * 100)
+    o = oracle.BamFile(blob)
+    S = split_kb * 1024
+    parts = oracle.load_reads_and_positions(o, S, reads_to_check=R)
+    sizes = [len(p) for p in parts]
+    offs = np.concatenate(parts).astype(np.int64)
+    assert np.array_equal(offs[-25:], o.L - 100 + 4 * np.arange(25))  # the zero "records" are in the partitions
+    with sbam.BamFile(blob, path="zeros_tail.bam") as g:
+        g.check_eager_device(0, g.uncompressed_size, R)
+        got_sizes, cols = g.load_records(S, reads_to_check=R, use_success_bitmap=True)
+        assert got_sizes.tolist() == sizes
+        check_columns(o, offs, cols)

@@ -166,3 +166,61 @@ class SynthBam:
 
     def bytes(self) -> np.ndarray:
         return self.slice(0, self.size)
+
+
+def bgzf_blocks(raw: bytes):
+    """(start, size, ISIZE) of every BGZF block of `raw` (BSIZE at +16, ISIZE in the last 4 bytes)."""
+    out, pos = [], 0
+    while pos + 18 <= len(raw):
+        n = (raw[pos + 16] | (raw[pos + 17] << 8)) + 1
+        out.append((pos, n, int.from_bytes(raw[pos + n - 4:pos + n], "little")))
+        pos += n
+    return out
+
+
+class TiledBam(SynthBam):
+    """A real BAM's data blocks repeated to a target size behind its header block (bench.py --real): the header block,
+    then the data blocks (every block after the header block up to the EOF marker) k times, then the EOF marker.  The
+    file must have a header-only first block and data blocks that start and end on record boundaries — true of the
+    reference's test_bams/src/main/resources/5k.bam (tests/fixtures/5k.bam: block 0 is the header, its .records file
+    starts every one of blocks 1..49 at offset 0), so the tiled stream is a valid BAM of real htsjdk-written
+    records whose record chain runs through every seam."""
+
+    def __init__(self, path: str, target_bytes: int):  # (SynthBam's generator is not used)
+        import zlib
+        raw = open(path, "rb").read()
+        blocks = bgzf_blocks(raw)
+        assert blocks[-1][2] == 0, "no EOF marker block"
+        h0, hn, _ = blocks[0]
+        self.header = np.frombuffer(raw[h0:h0 + hn], np.uint8).copy()
+        d0, d1 = blocks[1][0], blocks[-1][0]
+        self.tile = np.frombuffer(raw[d0:d1], np.uint8).copy()
+        self.eof = np.frombuffer(raw[d1:d1 + blocks[-1][1]], np.uint8).copy()
+        self.tail = np.zeros(0, np.uint8)
+        self.tail_records = 0
+        # header (Header.scala:26-60) and the records of one tile, from zlib
+        hx = raw[h0 + 18:h0 + hn - 8]
+        u = zlib.decompressobj(-15).decompress(hx)
+        p = 8 + int.from_bytes(u[4:8], "little")
+        n_ref = int.from_bytes(u[p:p + 4], "little")
+        p += 4
+        lens = []
+        for _ in range(n_ref):
+            ln = int.from_bytes(u[p:p + 4], "little")
+            lens.append(int.from_bytes(u[p + 4 + ln:p + 8 + ln], "little", signed=True))
+            p += 8 + ln
+        assert p == len(u), "the first block must hold exactly the header"
+        self.contig_lengths = np.array(lens, np.int64)
+        ut = b"".join(zlib.decompressobj(-15).decompress(raw[s + 18:s + n - 8]) for s, n, _ in blocks[1:-1])
+        x, nrec = 0, 0
+        while x < len(ut):
+            x += 4 + int.from_bytes(ut[x:x + 4], "little")
+            nrec += 1
+        assert x == len(ut), "the data blocks must end on a record boundary"
+        self.tile_records, self.tile_u = nrec, len(ut)
+        self.seed, self.read_len, self.level, self.tile_mb, self.threads = 0, -1, -1, self.tile.size / 2 ** 20, 1
+        self.distinct, self.cycle = False, 0
+        self.tiles, self.tiles_records = [self.tile], [nrec]
+        self.copies = max(1, round((target_bytes - self.header.size - 28) / self.tile.size))
+        self.path = path
+        self._sizes()
