@@ -148,6 +148,7 @@ class GpuShard:
         self.contig_lengths = np.asarray(contig_lengths, np.int64)
         self.device, self.halo, self.R = device, halo, reads_to_check
         self.f = None
+        self.retries = 0  # halo retries so far (each grows the halo 4x and re-runs the shard)
         self._open()
 
     def _open(self):
@@ -189,7 +190,11 @@ class GpuShard:
                 if self.plan.load_range(self.halo)[1] >= self.plan.file_size:
                     raise
                 self.halo *= 4
-                self._open()
+                self.retries += 1
+                # the grown range goes into the same context (sbam_load keeps its device allocations and only grows
+                # the ones the larger range needs), so a retry costs one H2D copy and the re-run, not a new context
+                lo, hi = self.plan.load_range(self.halo)
+                self.f.load(self.source(lo, hi), base_offset=lo, file_size=self.plan.file_size)
 
     def step(self) -> ShardResult:
         """compute-splits + full-check of the shard."""
