@@ -532,6 +532,7 @@ def main():
                        "file_gb": round(s.size / 1e9, 3), "uncompressed_gb_per_gpu": round(U / 1e9, 3),
                        "records": s.n_records, "blocks_per_gpu": nblocks, "split_mb": args.split_mb,
                        "windows_per_gpu": W, "parallelism": f"shard{world}",
+                       "halo_retries": int(shard.retries if W == 1 else sum(c.retries for c in pipe.ctx if c)),
                        "tiles": min(args.tiles, s.copies), "setup_s": round(setup_s, 1),
                        **({"contigs": len(s.contig_lengths)} if args.contigs else {})},
             "uncompressed_gbps": round(U * world * args.steps / elapsed / 1e9, 3),

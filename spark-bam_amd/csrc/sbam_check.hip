@@ -549,6 +549,7 @@ struct Tile {
   const uint32_t *opc;    // 4 × kOpcWords dwords (interleaved)
   const uint32_t *nbad;   // kNameWords dwords
   int64_t base;
+  const int32_t *nxt;     // stage_nxt: class r's first invalid op start at or after 256 k + r (r * kNxt + k)
 };
 
 // 64 bits of an LDS bitmap from bit x: two funnel shifts (v_alignbit), no branch on the bit offset
@@ -578,6 +579,149 @@ SB_DEV bool name_has_bad(const Tile &t, int rel, int32_t n) {
   return false;
 }
 
+// Long op arrays.  An op array whose first 64 ops are valid is rare in short-read data but the rule inside a long
+// read's packed sequence (nibbles 1, 2, 4, 8 are all valid op codes, and n_cigar there is >= 0x1111), so every
+// position of such a region asks for the first invalid op among thousands.  Per tile, stage_nxt keeps for each
+// residue class r the first invalid op start at or after 256 k + r (k < kNxt; kNoBad: none in the window), so a
+// window lookup is one 64-op bitmap read and one table read; past the window the stream is read 16 B at a time
+// (k_check_bits: by the whole wave, 8 KiB per step, once per tile and class).
+constexpr int kNxt = kWin / 256 + 1;
+constexpr int32_t kNoBad = 0x3fffffff;
+static_assert(kWin % 256 == 0 && kCheckThreads == 4 * 64, "stage_nxt: one wave per residue class");
+
+// Fill t.nxt (after stage_tile's bitmaps are complete): wave r computes class r, lane k super-chunk k, then a suffix
+// minimum across the lanes.
+SB_DEV void stage_nxt(const uint32_t *s_opc, int32_t *s_nxt) {
+  const int r = (int)(threadIdx.x >> 6), k = lane_id();
+  int32_t v = kNoBad;
+  if (k < kNxt - 1) {
+    const uint64_t m = op_bits(s_opc, 256 * k + r);
+    if (m) v = 256 * k + r + 4 * (int32_t)__builtin_ctzll(m);
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t u = __shfl_down(v, o, 64);
+    if (k + o < 64) v = min(v, u);
+  }
+  if (k < kNxt) s_nxt[r * kNxt + k] = v;
+}
+
+// The same table built by one wave for itself (its own LDS slice; wave-level ordering only), when a tile first needs
+// it: lanes k < kNxt take super-chunk k of all four classes.
+__attribute__((noinline)) __device__ void wave_nxt(const uint32_t *s_opc, int32_t *nx) {
+  const int k = lane_id();
+  int32_t v[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    v[r] = kNoBad;
+    if (k < kNxt - 1) {
+      const uint64_t m = op_bits(s_opc, 256 * k + r);
+      if (m) v[r] = 256 * k + r + 4 * (int32_t)__builtin_ctzll(m);
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int32_t u = __shfl_down(v[r], o, 64);
+      if (k + o < 64) v[r] = min(v[r], u);
+    }
+  }
+  if (k < kNxt)
+#pragma unroll
+    for (int r = 0; r < 4; r++) nx[r * kNxt + k] = v[r];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// First invalid op start (window-relative) at or after y (y's class), kNoBad if none before the window's end.
+SB_DEV int32_t next_bad_in_window(const Tile &t, int y) {
+  if (y >= kWin) return kNoBad;
+  const int r = y & 3, k = (y - r + 255) >> 8;  // table entry k covers class r from 256 k + r >= y
+  const int g = (256 * k + r - y) >> 2;         // the < 64 ops before it, from the bitmap
+  const uint64_t m = op_bits(t.opc, y) & ((1ull << g) - 1ull);
+  return m ? y + 4 * (int32_t)__builtin_ctzll(m) : t.nxt[r * kNxt + k];
+}
+
+// The first invalid op start of class r at or after the aligned position a (bytes [a, a + 16) of the stream), as a
+// 4-bit mask per class of the 16-B chunk: bit j of byte r = the op at a + 4 j + r is invalid.
+typedef unsigned int u32x4g __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4g *g16v;
+SB_DEV uint32_t bad_ops16(const u32x4g v) {
+  auto bad = [](uint32_t w) { return (((w & 0x0f0f0f0fu) + 0x07070707u) >> 4) & 0x01010101u; };
+  return bad(v.x) | bad(v.y) << 1 | bad(v.z) << 2 | bad(v.w) << 3;
+}
+
+// Wave-cooperative (every lane calls it with the same arguments): any invalid op among the n ops at c, c + 4, ...?
+// 4 KiB of the stream per step (4 loads of 16 B per lane in flight).  Reads stay within the interior's reach or the
+// stream's zero pad.
+SB_DEV bool ops_bad_wave(const StreamView &sv, int64_t c, int32_t n) {
+  const int r = (int)(c & 3), lane = lane_id();
+  const int64_t e = c + 4 * (int64_t)n, a0 = c & ~(int64_t)15;
+  const g16v src = (g16v)gview(sv.u);
+  for (int64_t a = a0; a < e; a += 4096) {
+    uint32_t m[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int64_t p = a + 1024 * k + 16 * lane;
+      m[k] = p < e ? (bad_ops16(src[p >> 4]) >> (8 * r)) & 0xfu : 0u;
+    }
+    bool hit = false;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int64_t p = a + 1024 * k + 16 * lane + r;  // op j of the chunk at p + 4 j
+#pragma unroll
+      for (int j = 0; j < 4; j++) hit |= ((m[k] >> j) & 1u) && p + 4 * j >= c && p + 4 * j < e;
+    }
+    if (__ballot(hit)) return true;
+  }
+  return false;
+}
+
+// Wave-cooperative: for each class r in `need`, nbe[r] (the wave's LDS) = the first invalid op start of class r at or
+// after A0 (16-B aligned), within kScanPast bytes (else kFarAway), kScanStep bytes per step.
+#ifndef SBAM_SCAN_STEP
+#define SBAM_SCAN_STEP 2048
+#endif
+constexpr int64_t kScanPast = 262144;  // >= the reach of any op array from a window (4 x 65535 ops)
+constexpr int64_t kFarAway = (int64_t)1 << 60;
+constexpr int kTableLanes = 8;  // k_check_bits: lanes of a wave in the long-op pass that make it build the table first
+constexpr int kScanStep = SBAM_SCAN_STEP;  // bytes per wave step (16 B per lane and load)
+__attribute__((noinline)) __device__ void scan_past_window(const StreamView &sv, int64_t A0, uint32_t need,
+                                                            int64_t *nbe) {
+  const int lane = lane_id();
+  const g16v src = (g16v)(gview(sv.u) + A0);
+  uint32_t left = need;
+  for (int it = 0; left && it < (int)(kScanPast / kScanStep); it++) {
+    uint32_t m[kScanStep / 1024];
+#pragma unroll
+    for (int i = 0; i < kScanStep / 1024; i++) m[i] = bad_ops16(src[(kScanStep / 16) * it + 64 * i + lane]);
+#pragma unroll
+    for (int i = 0; i < kScanStep / 1024; i++) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        if ((left >> r) & 1u) {
+          const uint64_t bal = __ballot(((m[i] >> (8 * r)) & 0xfu) != 0u);
+          if (bal) {
+            const int f = (int)__builtin_ctzll(bal);
+            const uint32_t mf = ((uint32_t)__builtin_amdgcn_readlane((int)m[i], f) >> (8 * r)) & 0xfu;
+            if (lane == 0) nbe[r] = A0 + kScanStep * (int64_t)it + 1024 * i + 16 * f + 4 * __builtin_ctz(mf) + r;
+            left &= ~(1u << r);
+          }
+        }
+      }
+    }
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+      if ((left >> r) & 1u) nbe[r] = kFarAway;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (the wave reads nbe[] back from LDS)
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Index of the first op among the first `lim` ops at c, c+4, ... whose first byte has (b & 0xf) > 8, or lim.
 SB_DEV int32_t first_bad_op(const Tile &t, const StreamView &sv, int64_t c, int32_t lim) {
   const int rel = (int)(c - t.base);
@@ -587,9 +731,22 @@ SB_DEV int32_t first_bad_op(const Tile &t, const StreamView &sv, int64_t c, int3
     return b < lim ? b : lim;
   }
   if (lim <= 64) return lim;
-  const gbytes u = gview(sv.u);  // > 64 valid ops in a row: rare, read on from HBM
-  for (int32_t i = 64; i < lim; i++)
-    if ((u[c + 4 * (int64_t)i] & 0xfu) > 8u) return i;
+  const int32_t p = next_bad_in_window(t, rel + 256);
+  if (p != kNoBad) return min((p - rel) >> 2, lim);
+  // past the window (this lane alone): aligned 64-B steps (4 loads in flight) from the window's end (the stream's
+  // zero pad covers reads past its end)
+  const int r = rel & 3;
+  const int64_t e = c + 4 * (int64_t)lim;
+  const g16v src = (g16v)gview(sv.u);
+  for (int64_t a = t.base + kWin; a < e; a += 64) {
+    uint32_t b4 = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) b4 |= ((bad_ops16(src[(a >> 4) + j]) >> (8 * r)) & 0xfu) << (4 * j);
+    if (b4) {
+      const int64_t q = a + 4 * __builtin_ctz(b4) + r;
+      return q < e ? (int32_t)((q - c) >> 2) : lim;
+    }
+  }
   return lim;
 }
 
@@ -938,6 +1095,7 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? kCheckWgsInt : kCheckWgs
   __shared__ uint32_t s_cnt[BYKEY ? 21 * 19 : 1];
   __shared__ uint32_t s_k12[3 * 19];    // keys 0-2 × flag (non-BYKEY modes)
   __shared__ uint32_t s_pair[19 * 19];  // close-call pairs (key 2)
+  __shared__ int32_t s_nxt[4 * kNxt];   // long op arrays (stage_nxt)
   const int lane = lane_id();
   for (int i = threadIdx.x; i < 3 * 19; i += kCheckThreads) s_k12[i] = 0;
   for (int i = threadIdx.x; i < 19 * 19; i += kCheckThreads) s_pair[i] = 0;
@@ -964,7 +1122,9 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? kCheckWgsInt : kCheckWgs
     __syncthreads();
     stage_tile(sv, base, s_win, s_opc, s_nbad);
     __syncthreads();
-    const Tile tl{s_win, s_opc, s_nbad, base};
+    stage_nxt(s_opc, s_nxt);
+    __syncthreads();
+    const Tile tl{s_win, s_opc, s_nbad, base, s_nxt};
     const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
     uint32_t hkp[3] = {0, 0, 0}, hpl[3] = {0, 0, 0};  // held compressed counts of an even group (add4_paired)
     constexpr bool TILECNT = MODE == MODE_COUNTS && PART == 2;  // boundary tiles of the bit-sliced pass
@@ -1129,6 +1289,88 @@ SB_DEV uint32_t ctz64(uint32_t lo, uint32_t hi) { return min(ffbl(lo), ffbl(hi) 
 // plane i of X[] holds flag kBitFlag[i] (the flags an interior position can fail)
 constexpr int kBitFlag[16] = {1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 13, 15, 16, 17, 18};
 
+// k_check_bits' op arrays of > 64 ops whose first 64 are valid (bits q of lane t's planes): the window's invalid-op
+// table, then the stream past the window, read once per tile and class by the whole wave (scan_past_window; nbe: the
+// wave's LDS slots; the table itself is built by the wave when a tile first needs it, wave_nxt).  A long read's packed
+// sequence puts every position here.  Wave-uniform call.
+// First invalid op start (window-relative) at or after y given that ops [y, y + 256) are valid (fb[y] >= 64), kNoBad
+// if none before the window's end: one more first-invalid-op byte, then the table (wave_nxt) from the next entry.
+SB_DEV int32_t next_bad_deep(const Tile &t, const uint8_t *fb, int y) {
+  const int y2 = y + 256;
+  if (y2 >= kWin) return kNoBad;
+  if (y2 >= kFbBytes) return next_bad_in_window(t, y2);
+  const uint32_t f = fb[y2];
+  if (f < 64u) return y2 + 4 * (int32_t)f;
+  const int r = y & 3, k = (y2 + 256 - r) >> 8;  // 256 k + r lies in (y2, y2 + 256]: the ops before it are valid
+  return t.nxt[r * kNxt + k];
+}
+
+SB_DEV uint32_t long_ops_pass(const Tile &tl, const uint8_t *fb, const StreamView &sv, uint32_t q, uint32_t pIV, int t,
+                              int64_t *nbe) {
+  auto at = [&](int b, int &crel, int32_t &nc) {  // bit b's op array: window-relative start, n_cigar
+    const int k = 31 - b, rel = 4 * ((k >> 2) * kCheckThreads + t) + (k & 3);
+    const int32_t lrn = tl.win[rel + 12];
+    nc = (int32_t)tl.win[rel + 16] | ((int32_t)tl.win[rel + 17] << 8);
+    crel = rel + 36 + (lrn >= 2 ? lrn : 0);
+  };
+  // ops 64 .. 127 from the first-invalid-op bytes (short-read data: the rare position here finds its invalid op
+  // there); a run that goes on ("deep") takes the wave's table, one that reaches the window's end ("past") the
+  // stream.  A wave with many lanes here is inside a long valid run (a long read's sequence): it builds the table
+  // first and resolves every position in one pass.
+  const bool table = __popcll(__ballot(q != 0u)) >= kTableLanes;
+  if (table) wave_nxt(tl.opc, const_cast<int32_t *>(tl.nxt));
+  uint32_t deep = 0, past = 0, cls = 0;
+  auto decide = [&](int b, int crel, int e, int32_t p) {
+    if (p != kNoBad) {
+      if (p < e) pIV |= 1u << b;
+    } else if (kWin < e) {
+      past |= 1u << b;
+      cls |= 1u << (crel & 3);
+    }
+  };
+  for (; q; q &= q - 1u) {
+    const int b = __builtin_ctz(q);
+    int crel;
+    int32_t nc;
+    at(b, crel, nc);
+    const int y = crel + 256, e = crel + 4 * nc;  // (ops 0-63 are valid: pIV is clear)
+    const uint32_t f = y < kFbBytes ? fb[y] : 64u;  // (>= 64: no invalid op among the 64 from y, or unknown)
+    if (f < 64u) {
+      if (y + 4 * (int)f < e) pIV |= 1u << b;
+    } else if (y >= kWin) {
+      decide(b, crel, e, kNoBad);
+    } else if (y >= kFbBytes) {
+      if (table) decide(b, crel, e, next_bad_in_window(tl, y));
+      else deep |= 1u << b;
+    } else if (y + 256 < e) {  // (else the 64 valid ops from y are the rest of the array)
+      if (table) decide(b, crel, e, next_bad_deep(tl, fb, y));
+      else deep |= 1u << b;
+    }
+  }
+  if (__ballot(deep != 0u)) {
+    wave_nxt(tl.opc, const_cast<int32_t *>(tl.nxt));
+    for (; deep; deep &= deep - 1u) {
+      const int b = __builtin_ctz(deep);
+      int crel;
+      int32_t nc;
+      at(b, crel, nc);
+      decide(b, crel, crel + 4 * nc, next_bad_in_window(tl, crel + 256));
+    }
+  }
+  const uint32_t need = wave_or(cls);
+  if (need) {
+    scan_past_window(sv, tl.base + kWin, need, nbe);
+    for (; past; past &= past - 1u) {
+      const int b = __builtin_ctz(past);
+      int crel;
+      int32_t nc;
+      at(b, crel, nc);
+      if (nbe[crel & 3] < tl.base + crel + 4 * (int64_t)nc) pIV |= 1u << b;
+    }
+  }
+  return pIV;
+}
+
 __global__ __launch_bounds__(kCheckThreads, kCheckWgsBits) void k_check_bits(StreamView sv, int64_t x0, int R,
                                                                                    CountsDev cd,
                                                                                    unsigned long long *__restrict__ bitmap,
@@ -1137,6 +1379,8 @@ __global__ __launch_bounds__(kCheckThreads, kCheckWgsBits) void k_check_bits(Str
   __shared__ uint32_t s_opc[4 * kOpcWords];
   __shared__ uint32_t s_nbad[kNameWords];
   __shared__ __attribute__((aligned(16))) uint8_t s_fb[kFbBytes];  // first invalid op from each byte (stage_fb)
+  __shared__ int32_t s_nxt[4][4 * kNxt];                            // long op arrays, per wave (wave_nxt)
+  __shared__ int64_t s_nbe[4][4];                                   // ... past the window, per wave and class
   // per lane and byte offset y of its 32: I(y) < -1, I(y) >= n_ref, 0 <= I(y) < n_ref && I(y + 4) > len[I(y)],
   // byte(y) == 0, byte(y) == 1, byte(y) > 64 (I(y): the int32 at y)
   __shared__ uint32_t s_pl[6][kCheckThreads + 8];
@@ -1282,7 +1526,7 @@ __global__ __launch_bounds__(kCheckThreads, kCheckWgsBits) void k_check_bits(Str
     }
     // the name characters matter only where the name ends in NUL (true records and ~1/256 of the rest): those
     // positions are checked one by one, and so are the op arrays longer than 64 ops whose first 64 are valid
-    const Tile tl{s_win, s_opc, s_nbad, base};
+    const Tile tl{s_win, s_opc, s_nbad, base, s_nxt[t >> 6]};
     const uint32_t HN = ~(pZ | pO);  // l_read_name >= 2
     uint32_t pNB = 0;
     for (uint32_t q = HN & pLZ; q; q &= q - 1u) {
@@ -1293,11 +1537,9 @@ __global__ __launch_bounds__(kCheckThreads, kCheckWgsBits) void k_check_bits(Str
       if (!bad && nbody > 64) bad = name_has_bad(tl, rel + 36 + 64, nbody - 64);
       pNB |= bad ? (1u << b) : 0u;
     }
-    for (uint32_t q = pNG & ~pIV; q; q &= q - 1u) {
-      const int b = __builtin_ctz(q), k = 31 - b, rel = 4 * ((k >> 2) * kCheckThreads + t) + (k & 3);
-      const int32_t lrn = s_win[rel + 12], nc = (int32_t)s_win[rel + 16] | ((int32_t)s_win[rel + 17] << 8);
-      if (first_bad_op(tl, sv, base + rel + 36 + (lrn >= 2 ? lrn : 0), nc) < nc) pIV |= 1u << b;
-    }
+    // (op arrays of > 64 ops whose first 64 are valid: the window's invalid-op table, then the stream past the window
+    // read once per tile and class by the whole wave — a long read's packed sequence puts every position here)
+    if (__ballot((pNG & ~pIV) != 0u)) pIV = long_ops_pass(tl, s_fb, sv, pNG & ~pIV, pIV, t, s_nbe[t >> 6]);
     // ---- flag planes
     uint32_t X[16];
     X[0] = s_pl[0][t + 1];          // 1  refIdx < -1
@@ -1415,30 +1657,33 @@ static_assert(kTile / 32 == 64 * 4, "k_eager_wave: the tile's bitmap is one u32x
 // eager.Checker record-0 checks at position rel of a wave's window (win = the tile's bytes from base), given the
 // fixed fields f[]: check_first<true, true>'s pass/fail, straight from the bytes (no op-class / name-character
 // bitmaps: survivors are few, and a true record's name and CIGAR are short).
-SB_DEV bool eager_pass_win(const uint8_t *win, const StreamView &sv, int64_t x, int rel, const int32_t f[8]) {
+// 0: fails; 1: passes; 2: passes so far, with the ops from 64 on (n64 of them at c64) left to a wave-cooperative read
+// (ops_bad_wave: a long read's CIGAR has thousands of ops).
+SB_DEV int eager_pass_win(const uint8_t *win, const StreamView &sv, int64_t x, int rel, const int32_t f[8],
+                          int64_t &c64, int32_t &n64) {
   const int32_t bs = f[0], ri = f[1], rp = f[2], bmn = f[3], fnc = f[4], ls = f[5], nri = f[6], nrp = f[7];
   const int32_t lrn = bmn & 0xff;
   const uint32_t flag = ((uint32_t)fnc) >> 16;
   const int32_t nc = fnc & 0xffff;
   if ((uint32_t)(lrn < 2) | (uint32_t)((flag & 4u) == 0 && (ls == 0 || nc == 0)) |
       (uint32_t)too_few_remaining(bs, lrn, nc, ls))
-    return false;
-  if (ref_err(ri, rp, nullptr, sv.lens, sv.nref) | ref_err(nri, nrp, nullptr, sv.lens, sv.nref)) return false;
+    return 0;
+  if (ref_err(ri, rp, nullptr, sv.lens, sv.nref) | ref_err(nri, nrp, nullptr, sv.lens, sv.nref)) return 0;
   const gbytes u = gview(sv.u);
   const int c0 = rel + 36 + lrn;
   if (c0 + 4 > kEwWin) {  // the name runs past the window (a position in the tile's last ~300 B): global memory
     typedef const __attribute__((address_space(1))) uint32_t *g32;
-    if (u[x + 35 + lrn] != 0) return false;
+    if (u[x + 35 + lrn] != 0) return 0;
     for (int i = 0; i < lrn - 1; i += 4) {
       const int64_t a = x + 36 + i;
       const g32 q = (g32)(u + (a & ~(int64_t)3));
       const uint32_t v = __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)a & 3u);
       const int left = lrn - 1 - i;
       const uint32_t keep = left >= 4 ? 0x80808080u : (0x80808080u >> (8 * (4 - left)));
-      if (name_bad_bytes(v) & keep) return false;
+      if (name_bad_bytes(v) & keep) return 0;
     }
   } else {
-    if (win[rel + 35 + lrn] != 0) return false;  // name not NUL-terminated
+    if (win[rel + 35 + lrn] != 0) return 0;  // name not NUL-terminated
     // allowedReadNameChars, 4 name bytes per step (SWAR over an unaligned dword of the window)
     const uint32_t *w32 = reinterpret_cast<const uint32_t *>(win);
     for (int i = 0; i < lrn - 1; i += 4) {
@@ -1446,15 +1691,21 @@ SB_DEV bool eager_pass_win(const uint8_t *win, const StreamView &sv, int64_t x, 
       const uint32_t w = __builtin_amdgcn_alignbyte(w32[(a >> 2) + 1], w32[a >> 2], (uint32_t)a & 3u);
       const int left = lrn - 1 - i;
       const uint32_t keep = left >= 4 ? 0x80808080u : (0x80808080u >> (8 * (4 - left)));
-      if (name_bad_bytes(w) & keep) return false;
+      if (name_bad_bytes(w) & keep) return 0;
     }
   }
-  const int in_win = max(0, min(nc, (kEwWin - c0) >> 2));  // ops inside the window, then global memory
+  const int n1 = min(nc, 64);
+  const int in_win = max(0, min(n1, (kEwWin - c0) >> 2));  // ops inside the window, then global memory
   for (int i = 0; i < in_win; i++)
-    if ((win[c0 + 4 * i] & 0xfu) > 8u) return false;
-  for (int i = in_win; i < nc; i++)
-    if ((u[x + 36 + lrn + 4 * (int64_t)i] & 0xfu) > 8u) return false;
-  return true;
+    if ((win[c0 + 4 * i] & 0xfu) > 8u) return 0;
+  for (int i = in_win; i < n1; i++)
+    if ((u[x + 36 + lrn + 4 * (int64_t)i] & 0xfu) > 8u) return 0;
+  if (nc > 64) {
+    c64 = x + 36 + lrn + 256;
+    n64 = nc - 64;
+    return 2;
+  }
+  return 1;
 }
 
 // lane l ← lane l + 1's v; lane 63 ← `last` (wave_shl1 DPP, the lane past the wave keeps the old value)
@@ -1532,13 +1783,28 @@ __global__ __launch_bounds__(64 * kEwWaves) void k_eager_wave(StreamView sv, int
       }
       wave_sync();
       const uint32_t nq = min((uint32_t)kEwQ, total - r0);
-      for (uint32_t i = (uint32_t)lane; i < nq; i += 64) {
-        const int rel = q[i];
-        const int o = rel & 3, d = rel >> 2;
-        int32_t f[8];
+      for (uint32_t i0 = 0; i0 < nq; i0 += 64) {
+        const uint32_t i = i0 + (uint32_t)lane;
+        int res = 1, rel = 0;
+        int64_t c64 = 0;
+        int32_t n64 = 0;
+        if (i < nq) {
+          rel = q[i];
+          const int o = rel & 3, d = rel >> 2;
+          int32_t f[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) f[k] = (int32_t)__builtin_amdgcn_alignbyte(w32[d + k + 1], w32[d + k], o);
-        if (!eager_pass_win(win, sv, base + rel, rel, f)) atomicAnd(&bm[rel >> 5], ~(1u << (rel & 31)));
+          for (int k = 0; k < 8; k++) f[k] = (int32_t)__builtin_amdgcn_alignbyte(w32[d + k + 1], w32[d + k], o);
+          res = eager_pass_win(win, sv, base + rel, rel, f, c64, n64);
+          if (res == 0) atomicAnd(&bm[rel >> 5], ~(1u << (rel & 31)));
+        }
+        // op arrays past 64 ops: the wave reads each one's remaining ops together
+        for (uint64_t pm = __ballot(res == 2); pm; pm &= pm - 1ull) {
+          const int fl = (int)__builtin_ctzll(pm);
+          const int64_t c = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(c64 >> 32), fl) << 32) |
+                                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)c64, fl));
+          const int32_t n = __builtin_amdgcn_readlane(n64, fl);
+          if (ops_bad_wave(sv, c, n) && lane == fl) atomicAnd(&bm[rel >> 5], ~(1u << (rel & 31)));
+        }
       }
       wave_sync();
     }

@@ -99,6 +99,21 @@ class TestLongReadsGpu:
         assert np.array_equal(got.by_key, c) and np.array_equal(got.positions, npos)
         assert np.array_equal(got.reads_before_error, rbe) and got.n_success == ns
 
+    @pytest.mark.parametrize("reads_to_check", [10, 1])
+    def test_counts_bit_sliced(self, g, long_file, reads_to_check):
+        """The report-mode Counts (k_check_bits over the interior tiles).  Inside a long read's packed sequence every
+        position reads n_cigar >= 0x1111 with valid ops (nibbles 1, 2, 4, 8), so the first invalid op lies thousands
+        of ops on, often past the tile's window: the per-tile invalid-op table and the wave's scan past the window
+        decide flag 15 there (before round 6 each such position read its ops one byte at a time: 8.4 s at 10 GB)."""
+        s, d, o = long_file
+        c, npos, rbe, ns = o.counts_parallel(0, o.L, reads_to_check, 8)
+        got, bits = g.check_full_counts(0, o.L, reads_to_check, want_bitmap=True)
+        assert np.array_equal(got.totals, c.sum(0)) and np.array_equal(got.by_key[:3], c[:3])
+        assert np.array_equal(got.positions, npos) and np.array_equal(got.reads_before_error, rbe)
+        assert got.n_success == ns and int(bits.sum()) == ns
+        if reads_to_check == 10:
+            assert np.array_equal(np.nonzero(bits)[0], o.record_chain(int(o.header_end), o.L))
+
     def test_eager_is_record_chain(self, g, long_file):
         s, d, o = long_file
         truth = o.record_chain(int(o.header_end), o.L)
