@@ -457,6 +457,7 @@ def main():
     # --- pinned host → results (SURVEY §8(d) "with H2D"): the same step with the shard's compressed bytes in
     # pinned host memory, streamed in `e2e_windows` windows through two contexts (window w+1's copy overlaps
     # window w's kernels; window 0's copy is not overlapped).
+    retries = int(shard.retries if W == 1 else sum(c.retries for c in pipe.ctx if c))
     e2e = None
     if args.e2e_windows > 0 and W == 1 and args.workload == "full-check":
         if shard is not None:
@@ -532,7 +533,7 @@ def main():
                        "file_gb": round(s.size / 1e9, 3), "uncompressed_gb_per_gpu": round(U / 1e9, 3),
                        "records": s.n_records, "blocks_per_gpu": nblocks, "split_mb": args.split_mb,
                        "windows_per_gpu": W, "parallelism": f"shard{world}",
-                       "halo_retries": int(shard.retries if W == 1 else sum(c.retries for c in pipe.ctx if c)),
+                       "halo_retries": retries,
                        "tiles": min(args.tiles, s.copies), "setup_s": round(setup_s, 1),
                        **({"contigs": len(s.contig_lengths)} if args.contigs else {})},
             "uncompressed_gbps": round(U * world * args.steps / elapsed / 1e9, 3),
