@@ -550,6 +550,7 @@ struct Tile {
   const uint32_t *nbad;   // kNameWords dwords
   int64_t base;
   const int32_t *nxt;     // stage_nxt: class r's first invalid op start at or after 256 k + r (r * kNxt + k)
+  int64_t *pw = nullptr;  // k_check: the wave's first invalid op start of class r past the window (-1: not read yet)
 };
 
 // 64 bits of an LDS bitmap from bit x: two funnel shifts (v_alignbit), no branch on the bit offset
@@ -733,21 +734,28 @@ SB_DEV int32_t first_bad_op(const Tile &t, const StreamView &sv, int64_t c, int3
   if (lim <= 64) return lim;
   const int32_t p = next_bad_in_window(t, rel + 256);
   if (p != kNoBad) return min((p - rel) >> 2, lim);
-  // past the window (this lane alone): aligned 64-B steps (4 loads in flight) from the window's end (the stream's
-  // zero pad covers reads past its end)
+  // past the window (this lane alone): the first invalid op start of the class at or after the window's end, read in
+  // aligned 64-B steps (4 loads in flight) up to the reach of any op array or the stream's end (its zero pad covers
+  // the last step), and kept for the wave's other positions in t.pw (lanes that race there store the same value)
   const int r = rel & 3;
   const int64_t e = c + 4 * (int64_t)lim;
-  const g16v src = (g16v)gview(sv.u);
-  for (int64_t a = t.base + kWin; a < e; a += 64) {
-    uint32_t b4 = 0;
+  int64_t q = t.pw ? t.pw[r] : -1;
+  if (q < 0) {
+    q = kFarAway;
+    const g16v src = (g16v)gview(sv.u);
+    const int64_t a0 = t.base + kWin, a1 = min(a0 + kScanPast, sv.L);
+    for (int64_t a = a0; a < a1; a += 64) {
+      uint32_t b4 = 0;
 #pragma unroll
-    for (int j = 0; j < 4; j++) b4 |= ((bad_ops16(src[(a >> 4) + j]) >> (8 * r)) & 0xfu) << (4 * j);
-    if (b4) {
-      const int64_t q = a + 4 * __builtin_ctz(b4) + r;
-      return q < e ? (int32_t)((q - c) >> 2) : lim;
+      for (int j = 0; j < 4; j++) b4 |= ((bad_ops16(src[(a >> 4) + j]) >> (8 * r)) & 0xfu) << (4 * j);
+      if (b4) {
+        q = a + 4 * __builtin_ctz(b4) + r;
+        break;
+      }
     }
+    if (t.pw) t.pw[r] = q;
   }
-  return lim;
+  return q < e ? (int32_t)((q - c) >> 2) : lim;
 }
 
 // PosChecker.getRefPosError bits with the contig length read unconditionally (clamped index) from LDS.
@@ -1096,6 +1104,7 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? kCheckWgsInt : kCheckWgs
   __shared__ uint32_t s_k12[3 * 19];    // keys 0-2 × flag (non-BYKEY modes)
   __shared__ uint32_t s_pair[19 * 19];  // close-call pairs (key 2)
   __shared__ int32_t s_nxt[4 * kNxt];   // long op arrays (stage_nxt)
+  __shared__ int64_t s_pw[4][4];        // ... past the window, per wave and class (first_bad_op)
   const int lane = lane_id();
   for (int i = threadIdx.x; i < 3 * 19; i += kCheckThreads) s_k12[i] = 0;
   for (int i = threadIdx.x; i < 19 * 19; i += kCheckThreads) s_pair[i] = 0;
@@ -1121,10 +1130,11 @@ __global__ __launch_bounds__(kCheckThreads, PART == 1 ? kCheckWgsInt : kCheckWgs
     const int64_t base = x0a + t * kTile;
     __syncthreads();
     stage_tile(sv, base, s_win, s_opc, s_nbad);
+    if (lane < 4) s_pw[threadIdx.x >> 6][lane] = -1;
     __syncthreads();
     stage_nxt(s_opc, s_nxt);
     __syncthreads();
-    const Tile tl{s_win, s_opc, s_nbad, base, s_nxt};
+    const Tile tl{s_win, s_opc, s_nbad, base, s_nxt, s_pw[threadIdx.x >> 6]};
     const uint32_t *w32 = reinterpret_cast<const uint32_t *>(s_win);
     uint32_t hkp[3] = {0, 0, 0}, hpl[3] = {0, 0, 0};  // held compressed counts of an even group (add4_paired)
     constexpr bool TILECNT = MODE == MODE_COUNTS && PART == 2;  // boundary tiles of the bit-sliced pass
