@@ -142,10 +142,10 @@ def data_desc(args, s) -> str:
 def pinned_digest(args, s):
     """The CPU oracle's digests of this exact file and split size (tests/golden/bench_digests.json, written by
     tests/golden/make_bench_digests.py at full size), or None when this workload was not pinned."""
-    if args.real or args.level != 6 or args.contigs or args.workload != "full-check":
+    if args.real or args.contigs or args.workload != "full-check":
         return None
     key = {"file_bytes": int(s.size), "seed": args.seed, "tile_mb": args.tile_mb, "tiles": args.tiles,
-           "read_len": args.read_len, "level": 6, "split_mb": args.split_mb, "reads_to_check": 10}
+           "read_len": args.read_len, "level": args.level, "split_mb": args.split_mb, "reads_to_check": 10}
     try:
         db = json.load(open(os.path.join(ROOT, "tests", "golden", "bench_digests.json")))
     except (OSError, ValueError):

@@ -22,6 +22,7 @@ FindRecordStart and the record chain in the window of the segment holding the sp
 
     python tests/golden/make_bench_digests.py --size-gb 10            # bench.py's default N=1 line
     python tests/golden/make_bench_digests.py --size-gb 3.75 --world 8 # configs[2]: 30 GB, --gpus 8 --size-gb 3.75
+    python tests/golden/make_bench_digests.py --size-gb 10 --level 0   # bench.py --level 0 (stored blocks)
 """
 from __future__ import annotations
 
@@ -53,7 +54,7 @@ N_COUNT_WORDS = 19 + 21 * 19 + 21 + 21 * 128 + 19 * 19 + 3
 def workload_key(s, args) -> dict:
     """What identifies the file and the run: the bytes (generator arguments and exact size) and the split size."""
     return {"file_bytes": int(s.size), "seed": args.seed, "tile_mb": args.tile_mb, "tiles": args.tiles,
-            "read_len": args.read_len, "level": 6, "split_mb": args.split_mb, "reads_to_check": 10}
+            "read_len": args.read_len, "level": args.level, "split_mb": args.split_mb, "reads_to_check": 10}
 
 
 def lib():
@@ -124,6 +125,7 @@ def parser():
     ap.add_argument("--tiles", type=int, default=16)
     ap.add_argument("--seed", type=lambda x: int(x, 0), default=0x5EEDBA11)
     ap.add_argument("--read-len", type=int, default=150)
+    ap.add_argument("--level", type=int, default=6, help="zlib level of the synthetic blocks (bench.py --level)")
     ap.add_argument("--split-mb", type=float, default=2.0)
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
     ap.add_argument("--halo-mb", type=float, default=HALO / (1 << 20))
@@ -138,7 +140,8 @@ def pin(args) -> dict:
     L = lib()
     t_all = time.time()
     s = synth.SynthBam.for_size(int(args.size_gb * 1e9 * args.world), tile_mb=args.tile_mb, seed=args.seed, threads=T,
-                                read_len=args.read_len, distinct=args.tiles > 1, cycle=max(args.tiles, 1))
+                                read_len=args.read_len, level=args.level, distinct=args.tiles > 1,
+                                cycle=max(args.tiles, 1))
     segs = segments(s)
     print(f"file {s.size} B, {s.n_records} records, {len(segs)} segments", flush=True)
 
@@ -271,7 +274,8 @@ def pin(args) -> dict:
            "splits": hashlib.sha1(rows.ravel().tobytes()).hexdigest()[:16], "n_splits": len(hsplits)}
     entry = {"workload": workload_key(s, args), "digest": dig, "records": s.n_records, "n_success": int(scal[0]),
              "uncompressed_bytes": U, "made_by": f"tests/golden/make_bench_digests.py --size-gb {args.size_gb:g} "
-             f"--world {args.world}", "oracle_wall_s": round(time.time() - t_all, 1), "threads": T}
+             f"--world {args.world}" + (f" --level {args.level}" if args.level != 6 else ""),
+             "oracle_wall_s": round(time.time() - t_all, 1), "threads": T}
     print(json.dumps(entry), flush=True)
     return entry
 

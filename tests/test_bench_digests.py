@@ -12,6 +12,7 @@ import os
 import sys
 
 import numpy as np
+import pytest
 
 from conftest import GOLDEN
 
@@ -40,13 +41,16 @@ def whole_file_digests(s, split_size):
             "splits": hashlib.sha1(rows.ravel().tobytes()).hexdigest()[:16], "n_splits": len(parts)}
 
 
-def test_segmented_pin_equals_whole_file_oracle():
+@pytest.mark.parametrize("level", [6, 0])
+def test_segmented_pin_equals_whole_file_oracle(level):
+    """level 0: bench.py --level 0's stored blocks (one pin per level)."""
     import synth
     args = argparse.Namespace(size_gb=0.03, world=2, tile_mb=4.0, tiles=3, seed=0x5EEDBA11, read_len=150,
-                              split_mb=1.0, threads=8, halo_mb=2.0, out="")
+                              split_mb=1.0, threads=8, halo_mb=2.0, out="", level=level)
     got = mbd.pin(args)
+    assert got["workload"]["level"] == level
     s = synth.SynthBam.for_size(int(args.size_gb * 1e9 * args.world), tile_mb=args.tile_mb, seed=args.seed, threads=8,
-                                read_len=150, distinct=True, cycle=args.tiles)
+                                read_len=150, level=level, distinct=True, cycle=args.tiles)
     assert got["workload"]["file_bytes"] == s.size and s.copies > args.tiles  # cycled tiles, several windows
     assert got["digest"] == whole_file_digests(s, int(args.split_mb * (1 << 20)))
 
@@ -58,6 +62,7 @@ def test_committed_pins_cover_the_headline_workloads():
         w = e["workload"]
         assert set(e["digest"]) == {"counts", "splits", "n_splits"} and e["n_success"] == e["records"]
         assert (w["seed"], w["tile_mb"], w["tiles"], w["read_len"], w["split_mb"]) == (0x5EEDBA11, 64.0, 16, 150, 2.0)
+        assert w["level"] in (0, 1, 6)
         by_size[e["made_by"]] = e
     made = " ".join(by_size)
     assert "--size-gb 10 --world 1" in made  # configs[1]: bench.py's N=1 line
