@@ -682,13 +682,11 @@ SB_DEV bool ops_bad_wave(const StreamView &sv, int64_t c, int32_t n) {
 
 // Wave-cooperative: for each class r in `need`, nbe[r] (the wave's LDS) = the first invalid op start of class r at or
 // after A0 (16-B aligned), within kScanPast bytes (else kFarAway), kScanStep bytes per step.
-#ifndef SBAM_SCAN_STEP
-#define SBAM_SCAN_STEP 2048
-#endif
 constexpr int64_t kScanPast = 262144;  // >= the reach of any op array from a window (4 x 65535 ops)
 constexpr int64_t kFarAway = (int64_t)1 << 60;
 constexpr int kTableLanes = 8;  // k_check_bits: lanes of a wave in the long-op pass that make it build the table first
-constexpr int kScanStep = SBAM_SCAN_STEP;  // bytes per wave step (16 B per lane and load)
+constexpr int kScanStep = 2048;  // bytes per wave step, 16 B per lane and load (8 KiB: the loads' 32 VGPRs spilled
+                                 // k_check_bits' record loop)
 __attribute__((noinline)) __device__ void scan_past_window(const StreamView &sv, int64_t A0, uint32_t need,
                                                             int64_t *nbe) {
   const int lane = lane_id();
