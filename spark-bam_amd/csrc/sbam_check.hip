@@ -685,8 +685,7 @@ SB_DEV bool ops_bad_wave(const StreamView &sv, int64_t c, int32_t n) {
 constexpr int64_t kScanPast = 262144;  // >= the reach of any op array from a window (4 x 65535 ops)
 constexpr int64_t kFarAway = (int64_t)1 << 60;
 constexpr int kTableLanes = 8;  // k_check_bits: lanes of a wave in the long-op pass that make it build the table first
-constexpr int kScanStep = 2048;  // bytes per wave step, 16 B per lane and load (8 KiB: the loads' 32 VGPRs spilled
-                                 // k_check_bits' record loop)
+constexpr int kScanStep = 2048;  // bytes per wave step: two 16-B loads per lane in flight
 __attribute__((noinline)) __device__ void scan_past_window(const StreamView &sv, int64_t A0, uint32_t need,
                                                             int64_t *nbe) {
   const int lane = lane_id();
