@@ -52,6 +52,13 @@ struct sbam_ctx {
   size_t bcap[5] = {0, 0, 0, 0, 0};
   std::vector<int64_t> h_bstart, h_buoff;
   std::vector<int32_t> h_bc, h_bu;
+  // the fast scan's table comes back behind the GPU, into pinned staging (the stream's length first, then the
+  // columns); host_blocks() moves it into h_* when the host first reads them (sbam_inflate: while the decoder runs)
+  uint8_t *h_stage = nullptr;
+  size_t stage_cap = 0;
+  hipEvent_t blk_ev[3] = {nullptr, nullptr, nullptr};  // [0]: the length copied, [1]: the columns copied, [2]: built
+  hipStream_t copy_stream = nullptr;  // the columns' copy runs here, beside the decoder
+  bool blk_pending = false;
   // uncompressed stream
   uint8_t *d_u = nullptr;
   size_t u_cap = 0;
@@ -69,6 +76,7 @@ struct sbam_ctx {
   int64_t bm_x0 = 0, bm_x1 = 0;
   bool bm_valid = false;
   bool bm_list = false;  // the bitmap came from the list-form chain pass: d_nfb[1..2] describe its links
+  int64_t plist_n = 0;   // (and d_plist[0, plist_n) its PASS0 positions)
   int32_t bm_R = -1;
   // inflate scratch: token pages of the decode → resolve path
   uint8_t *d_pool = nullptr;  // main token regions (inflate_token_bytes)
@@ -199,14 +207,39 @@ int no_read_found(sbam_ctx *c, int64_t start, int32_t max_read_size) {
                  max_read_size, c->path.c_str(), (long long)start);
 }
 
+// h_* of a table whose copy the fast scan left in flight (sbam_scan_blocks)
+int host_blocks(sbam_ctx *c) {
+  if (!c->blk_pending) return SBAM_OK;
+  HIPCHK(c, hipEventSynchronize(c->blk_ev[1]));
+  const int64_t nb = c->nblocks;
+  const int64_t *st = reinterpret_cast<const int64_t *>(c->h_stage + 8), *uo = st + nb;
+  const int32_t *cs = reinterpret_cast<const int32_t *>(uo + nb + 1), *us = cs + nb;
+  c->h_bstart.assign(st, st + nb);
+  c->h_buoff.assign(uo, uo + nb + 1);
+  c->h_bc.assign(cs, cs + nb);
+  c->h_bu.assign(us, us + nb);
+  c->blk_pending = false;
+  return SBAM_OK;
+}
+// the scanned stream's uncompressed length (waits only for its own 8-byte copy)
+int block_total(sbam_ctx *c, int64_t *L) {
+  if (!c->blk_pending) {
+    *L = c->h_buoff[c->nblocks];
+    return SBAM_OK;
+  }
+  HIPCHK(c, hipEventSynchronize(c->blk_ev[0]));
+  *L = *reinterpret_cast<const int64_t *>(c->h_stage);
+  return SBAM_OK;
+}
+// a scanned block table, with its host copy in h_*
 int ensure_blocks(sbam_ctx *c) {
   if (c->nblocks < 0) return set_err(c, SBAM_ERR_STATE, "sbam_scan_blocks has not run");
-  return SBAM_OK;
+  return host_blocks(c);
 }
 int ensure_stream(sbam_ctx *c) {
   if (c->L < 0) return set_err(c, SBAM_ERR_STATE, "sbam_inflate has not run");
   if (c->nref < 0) return set_err(c, SBAM_ERR_STATE, "contig lengths unknown (sbam_header / sbam_set_contig_lengths)");
-  return SBAM_OK;
+  return host_blocks(c);
 }
 
 // block index whose (relative) start == q, or -1
@@ -215,10 +248,23 @@ int64_t block_at(const sbam_ctx *c, int64_t q) {
   if (it == c->h_bstart.end() || *it != q) return -1;
   return it - c->h_bstart.begin();
 }
-sbam_pos pos_of(const sbam_ctx *c, int64_t x) {
-  // last block with uoff <= x and usize > 0 containing x; x at a block end normalises to (next, 0)
-  auto it = std::upper_bound(c->h_buoff.begin(), c->h_buoff.begin() + c->nblocks, x);
+sbam_pos pos_of(const sbam_ctx *c, int64_t x, int64_t *hint = nullptr) {
+  // last block with uoff <= x and usize > 0 containing x; x at a block end normalises to (next, 0).  hint: the block
+  // of the previous (smaller) query — the search gallops from it (split starts ascend: 4767 full binary searches
+  // over a 3 MB table were 0.2 ms of host time per 10 GB step)
+  int64_t lo = 0, hi = c->nblocks;
+  if (hint && *hint >= 0 && *hint < c->nblocks && c->h_buoff[*hint] <= x) {
+    int64_t step = 1;
+    lo = *hint;
+    while (lo + step < c->nblocks && c->h_buoff[lo + step] <= x) {
+      lo += step;
+      step *= 2;
+    }
+    hi = std::min(lo + step, c->nblocks);
+  }
+  auto it = std::upper_bound(c->h_buoff.begin() + lo, c->h_buoff.begin() + hi, x);
   int64_t b = (it - c->h_buoff.begin()) - 1;
+  if (hint && b >= 0) *hint = b;
   while (b >= 0 && b < c->nblocks && x >= c->h_buoff[b] + c->h_bu[b]) b++;
   if (b < 0 || b >= c->nblocks) {
     const int64_t endp = c->nblocks > 0 ? c->h_bstart[c->nblocks - 1] + c->h_bc[c->nblocks - 1] : 0;
@@ -310,6 +356,11 @@ void sbam_close(sbam_ctx *c) {
   }
   for (hipEvent_t e : c->load_ev)
     if (e) (void)hipEventDestroy(e);
+  if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+  for (hipEvent_t e : c->blk_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+  if (c->h_stage) (void)hipHostFree(c->h_stage);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -357,6 +408,7 @@ int sbam_reserve(sbam_ctx *c, int64_t comp_bytes, int64_t n_blocks, int64_t ubyt
   if (!c || comp_bytes < 0 || n_blocks < 0 || ubytes < 0 || n_records < 0) return SBAM_ERR_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->copy_stream) HIPCHK(c, hipStreamSynchronize(c->copy_stream));
   // Any stage buffer that grows is a fresh allocation whose contents are gone, so a context that has already run a
   // stage drops its stages (sbam_reset) when one grows: a later query re-runs them instead of reading uninitialised
   // device memory.  The resident compressed bytes and the contig lengths are kept.
@@ -383,7 +435,7 @@ int sbam_reserve(sbam_ctx *c, int64_t comp_bytes, int64_t n_blocks, int64_t ubyt
   HIPCHK(c, grow(&c->d_bh, &c->bcap[1], n_blocks + 1));
   HIPCHK(c, grow(&c->d_bc, &c->bcap[2], n_blocks + 1));
   HIPCHK(c, grow(&c->d_bu, &c->bcap[3], n_blocks + 1));
-  HIPCHK(c, grow(&c->d_buoff, &c->bcap[4], n_blocks + 1));
+  HIPCHK(c, grow(&c->d_buoff, &c->bcap[4], n_blocks + 1 + (n_blocks + 255) / 256));  // (+ the scan's sums)
   HIPCHK(c, grow(&c->d_u, &c->u_cap, (size_t)ubytes + kStreamPad));
   HIPCHK(c, grow(&c->d_status, &c->status_cap, n_blocks));
   HIPCHK(c, grow(&c->d_found, &c->found_cap, n_blocks));
@@ -415,6 +467,7 @@ int sbam_reset(sbam_ctx *c) {
   if (!c) return SBAM_ERR_ARG;
   c->ncand = -1;
   c->nblocks = -1;
+  c->blk_pending = false;
   c->L = -1;
   c->inflate_slow = -1;
   c->bm_valid = false;
@@ -530,19 +583,43 @@ int sbam_scan_blocks(sbam_ctx *c, int64_t *n_blocks) {
   c->h_bstart.clear();
   c->h_bc.clear();
   c->h_bu.clear();
+  if (c->copy_stream) HIPCHK(c, hipEventSynchronize(c->blk_ev[1]));  // (the last table's copy has read its columns)
   HIPCHK(c, ensure(&c->d_bstart, &c->bcap[0], nb + 1));
   HIPCHK(c, ensure(&c->d_bh, &c->bcap[1], nb + 1));
   HIPCHK(c, ensure(&c->d_bc, &c->bcap[2], nb + 1));
   HIPCHK(c, ensure(&c->d_bu, &c->bcap[3], nb + 1));
   if (fast) {
-    HIPCHK(c, launch_gather_blocks(c->d_cand, first, nb, c->d_bstart, c->d_bh, c->d_bc, c->d_bu, c->stream));
-    c->h_bstart.resize(nb);
-    c->h_bc.resize(nb);
-    c->h_bu.resize(nb);
-    HIPCHK(c, hipMemcpyAsync(c->h_bstart.data(), c->d_bstart, nb * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->h_bc.data(), c->d_bc, nb * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->h_bu.data(), c->d_bu, nb * 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    // columns and offsets built on the device; the host's copy is queued behind them, not waited for
+    const int64_t nwg = (nb + 255) / 256;
+    HIPCHK(c, ensure(&c->d_buoff, &c->bcap[4], nb + 1 + nwg));
+    HIPCHK(c, launch_gather_blocks(c->d_cand, first, nb, c->d_bstart, c->d_bh, c->d_bc, c->d_bu, c->d_buoff + nb + 1,
+                                   c->d_buoff, c->stream));
+    const size_t need = 8 + (size_t)nb * 8 + (size_t)(nb + 1) * 8 + (size_t)nb * 8;
+    if (c->stage_cap < need) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));  // (an earlier table's copy may still target the old staging)
+      if (c->h_stage) (void)hipHostFree(c->h_stage);
+      c->h_stage = nullptr;
+      c->stage_cap = 0;
+      HIPCHK(c, hipHostMalloc(reinterpret_cast<void **>(&c->h_stage), need + need / 8, hipHostMallocDefault));
+      c->stage_cap = need + need / 8;
+    }
+    for (hipEvent_t &e : c->blk_ev)
+      if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    if (!c->copy_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    int64_t *st = reinterpret_cast<int64_t *>(c->h_stage + 8), *uo = st + nb;
+    int32_t *cs = reinterpret_cast<int32_t *>(uo + nb + 1), *us = cs + nb;
+    HIPCHK(c, hipMemcpyAsync(c->h_stage, c->d_buoff + nb, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipEventRecord(c->blk_ev[0], c->stream));
+    HIPCHK(c, hipEventRecord(c->blk_ev[2], c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->blk_ev[2], 0));
+    HIPCHK(c, hipMemcpyAsync(uo, c->d_buoff, (nb + 1) * 8, hipMemcpyDeviceToHost, c->copy_stream));
+    if (nb) {
+      HIPCHK(c, hipMemcpyAsync(st, c->d_bstart, nb * 8, hipMemcpyDeviceToHost, c->copy_stream));
+      HIPCHK(c, hipMemcpyAsync(cs, c->d_bc, nb * 4, hipMemcpyDeviceToHost, c->copy_stream));
+      HIPCHK(c, hipMemcpyAsync(us, c->d_bu, nb * 4, hipMemcpyDeviceToHost, c->copy_stream));
+    }
+    HIPCHK(c, hipEventRecord(c->blk_ev[1], c->copy_stream));
+    c->blk_pending = true;
   } else {
     std::vector<Candidate> hc(c->ncand);
     HIPCHK(c, hipMemcpy(hc.data(), c->d_cand, c->ncand * sizeof(Candidate), hipMemcpyDeviceToHost));
@@ -569,17 +646,17 @@ int sbam_scan_blocks(sbam_ctx *c, int64_t *n_blocks) {
     HIPCHK(c, hipMemcpy(c->d_bh, h_h.data(), nb * 4, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_bc, c->h_bc.data(), nb * 4, hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_bu, c->h_bu.data(), nb * 4, hipMemcpyHostToDevice));
+    c->h_buoff.resize(nb + 1);
+    int64_t acc = 0;
+    for (int64_t b = 0; b < nb; b++) {
+      c->h_buoff[b] = acc;
+      acc += (c->h_bu[b] < 0) ? 0 : c->h_bu[b];
+    }
+    c->h_buoff[nb] = acc;
+    HIPCHK(c, ensure(&c->d_buoff, &c->bcap[4], nb + 1));
+    HIPCHK(c, hipMemcpyAsync(c->d_buoff, c->h_buoff.data(), (nb + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
   }
-  c->h_buoff.resize(nb + 1);
-  int64_t acc = 0;
-  for (int64_t b = 0; b < nb; b++) {
-    c->h_buoff[b] = acc;
-    acc += (c->h_bu[b] < 0) ? 0 : c->h_bu[b];
-  }
-  c->h_buoff[nb] = acc;
-  HIPCHK(c, ensure(&c->d_buoff, &c->bcap[4], nb + 1));
-  HIPCHK(c, hipMemcpyAsync(c->d_buoff, c->h_buoff.data(), (nb + 1) * 8, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
   c->nblocks = nb;
   if (n_blocks) *n_blocks = nb;
   return SBAM_OK;
@@ -601,10 +678,12 @@ int sbam_get_blocks(sbam_ctx *c, int64_t *start, int32_t *csize, int32_t *usize,
 
 int sbam_inflate(sbam_ctx *c, int64_t *usz) {
   if (!c) return SBAM_ERR_ARG;
-  int rc = ensure_blocks(c);
-  if (rc) return rc;
+  if (c->nblocks < 0) return set_err(c, SBAM_ERR_STATE, "sbam_scan_blocks has not run");
+  int rc = SBAM_OK;  // (the table's host copy is picked up below, while the decoder runs)
   HIPCHK(c, hipSetDevice(c->device));
-  const int64_t L = c->h_buoff[c->nblocks];
+  int64_t L = 0;
+  rc = block_total(c, &L);
+  if (rc) return rc;
   HIPCHK(c, ensure(&c->d_u, &c->u_cap, (size_t)L + kStreamPad));
   HIPCHK(c, hipMemsetAsync(c->d_u + L, 0, kStreamPad, c->stream));
   const int64_t nb = c->nblocks;
@@ -639,6 +718,10 @@ int sbam_inflate(sbam_ctx *c, int64_t *usz) {
       // (the slow list is consumed by now: the resolver's redo list reuses d_slow, its count is d_icnt[2])
       HIPCHK(c, launch_inflate_resolve(bt, c->d_u, tp, d_found, nullptr, 0, c->d_slow, c->d_icnt + 2, c->stream));
     }
+    // the table's host copy, while the kernels run (before the copies of the results below: copies into pageable
+    // memory wait for the stream)
+    rc = host_blocks(c);
+    if (rc) return rc;
     HIPCHK(c, hipMemcpyAsync(c->d_small + 2, &none, 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, launch_first_error(d_status, nb, reinterpret_cast<unsigned long long *>(c->d_small + 2), c->stream));
     HIPCHK(c, hipMemcpyAsync(&ferr, c->d_small + 2, 8, hipMemcpyDeviceToHost, c->stream));
@@ -729,6 +812,7 @@ int sbam_header(sbam_ctx *c, int32_t *n_ref, int64_t *lengths, int32_t cap, sbam
   if (!c) return SBAM_ERR_ARG;
   if (c->L < 0) return set_err(c, SBAM_ERR_STATE, "sbam_inflate has not run");
   if (c->base != 0) return set_err(c, SBAM_ERR_STATE, "header lives in the file's first block (shard: sbam_set_contig_lengths)");
+  if (int rc = host_blocks(c)) return rc;
   auto rd = [&](int64_t off, int64_t n, void *dst) -> bool {
     if (off < 0 || off + n > c->L) return false;
     return hipMemcpy(dst, c->d_u + off, (size_t)n, hipMemcpyDeviceToHost) == hipSuccess;
@@ -868,6 +952,7 @@ static hipError_t run_chains(sbam_ctx *c, int64_t x0, int64_t x1, int32_t R, int
   cs.fb = c->d_pfb;
   cs.n_fb = c->d_nfb;
   c->bm_list = true;
+  c->plist_n = total;
   return launch_chain_list_run(view(c), x0, x1, R, by_key, cd, c->d_bitmap, cs, c->stream);
 }
 
@@ -1073,7 +1158,8 @@ static int split_counts(sbam_ctx *c, bool try_bitmap, const std::vector<int64_t>
     const bool force = fp && *fp && *fp != '0';
     HIPCHK(c, launch_chain_proof(c->d_u, c->L, c->d_bitmap, xa, X0, X1, d_fail,
                                  (c->bm_list && !force) ? c->d_nfb : nullptr, c->stream));
-    HIPCHK(c, launch_split_popcounts(c->d_bitmap, xa, c->d_sx, c->d_se, n, c->d_sn, d_fail, c->stream));
+    HIPCHK(c, launch_split_popcounts(c->d_bitmap, xa, c->d_sx, c->d_se, n, c->d_sn, d_fail, c->d_plist, c->plist_n,
+                                     c->bm_list ? c->d_nfb : nullptr, c->stream));
     int32_t fail = 1;
     HIPCHK(c, hipMemcpyAsync(&fail, d_fail, 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(cnt.data(), c->d_sn, n * 8, hipMemcpyDeviceToHost, c->stream));
@@ -1105,8 +1191,9 @@ int sbam_split_records(sbam_ctx *c, const sbam_split_args *a, int64_t first, int
   bool proved = false;
   rc = split_counts(c, a->use_success_bitmap != 0, xs, xe, cnt, &proved);
   if (rc) return rc;
+  int64_t hint = 0;
   for (int64_t i = 0; i < count; i++) {
-    if (first_pos) first_pos[i] = pos_of(c, xs[i]);
+    if (first_pos) first_pos[i] = pos_of(c, xs[i], &hint);
     if (found) found[i] = cnt[i] > 0;
     if (n_records) n_records[i] = cnt[i];
   }

@@ -319,15 +319,57 @@ __global__ void k_lower_bound(const Candidate *__restrict__ c, int64_t n, int64_
   *out = cand_lower_bound(c, 0, n, q);
 }
 
-__global__ void k_gather_blocks(const Candidate *__restrict__ c, int64_t first, int64_t n, int64_t *__restrict__ st,
-                                int32_t *__restrict__ hs, int32_t *__restrict__ cs, int32_t *__restrict__ us) {
+SB_DEV int64_t wave_sum64(int64_t v) {
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// The block table's columns from the verified chain, plus each workgroup's sum of uncompressed sizes for
+// k_block_uoff (a negative isize counts 0, as MetadataStream's offsets do).
+__global__ __launch_bounds__(256) void k_gather_blocks(const Candidate *__restrict__ c, int64_t first, int64_t n,
+                                                       int64_t *__restrict__ st, int32_t *__restrict__ hs,
+                                                       int32_t *__restrict__ cs, int32_t *__restrict__ us,
+                                                       int64_t *__restrict__ wsum) {
+  __shared__ int64_t s[4];
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const Candidate ci = c[first + i];
-  st[i] = ci.pos;
-  hs[i] = ci.hsize;
-  cs[i] = ci.csize;
-  us[i] = ci.isize;
+  int64_t u = 0;
+  if (i < n) {
+    const Candidate ci = c[first + i];
+    st[i] = ci.pos;
+    hs[i] = ci.hsize;
+    cs[i] = ci.csize;
+    us[i] = ci.isize;
+    u = ci.isize < 0 ? 0 : ci.isize;
+  }
+  u = wave_sum64(u);
+  if (lane_id() == 0) s[threadIdx.x >> 6] = u;
+  __syncthreads();
+  if (threadIdx.x == 0) wsum[blockIdx.x] = s[0] + s[1] + s[2] + s[3];
+}
+
+// Uncompressed offsets uoff[0..n] (exclusive prefix of the sizes; uoff[n] = the stream's length): each workgroup adds
+// up the sums of the workgroups before it (n / 256 of them at most, from L2), then scans its own 256 blocks.
+__global__ __launch_bounds__(256) void k_block_uoff(const int32_t *__restrict__ us, int64_t n,
+                                                    const int64_t *__restrict__ wsum, int64_t *__restrict__ uoff) {
+  __shared__ int64_t s[8];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int64_t b = 0;
+  for (int64_t k = t; k < (int64_t)blockIdx.x; k += 256) b += wsum[k];
+  b = wave_sum64(b);
+  if (lane == 0) s[w] = b;
+  const int64_t i = (int64_t)blockIdx.x * 256 + t;
+  const int64_t v = i < n ? (us[i] < 0 ? 0 : us[i]) : 0;
+  int64_t x = v;  // inclusive scan within the wave
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s[4 + w] = x;
+  __syncthreads();
+  int64_t base = s[0] + s[1] + s[2] + s[3];
+  for (int k = 0; k < w; k++) base += s[4 + k];
+  if (i < n) uoff[i] = base + x - v;
+  if (i == n - 1) uoff[n] = base + x;
 }
 
 // ================================================================================================
@@ -385,9 +427,11 @@ hipError_t launch_lower_bound(const Candidate *c, int64_t n, int64_t q, int64_t 
   return hipGetLastError();
 }
 hipError_t launch_gather_blocks(const Candidate *c, int64_t first, int64_t n, int64_t *st, int32_t *hs, int32_t *cs,
-                                int32_t *us, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_gather_blocks, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, c, first, n, st, hs, cs, us);
+                                int32_t *us, int64_t *wsum, int64_t *uoff, hipStream_t s) {
+  if (n == 0) return hipMemsetAsync(uoff, 0, sizeof(int64_t), s);
+  const unsigned nwg = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(k_gather_blocks, dim3(nwg), dim3(256), 0, s, c, first, n, st, hs, cs, us, wsum);
+  hipLaunchKernelGGL(k_block_uoff, dim3(nwg), dim3(256), 0, s, us, n, wsum, uoff);
   return hipGetLastError();
 }
 }  // namespace sbam

@@ -88,8 +88,9 @@ hipError_t launch_chain_verify(const Candidate *cands, int64_t ncand, int64_t fi
 hipError_t launch_find_block_starts(const uint8_t *d, int64_t D, const Candidate *cands, int64_t ncand,
                                     const int64_t *starts, int64_t n, int32_t blocks_to_check, int64_t *out,
                                     hipStream_t s);
+// (+ uoff[0..n]: the uncompressed offsets, computed on the device; wsum: (n + 255) / 256 int64 of scratch)
 hipError_t launch_gather_blocks(const Candidate *cands, int64_t first, int64_t n, int64_t *start, int32_t *hsize,
-                                int32_t *csize, int32_t *usize, hipStream_t s);
+                                int32_t *csize, int32_t *usize, int64_t *wsum, int64_t *uoff, hipStream_t s);
 // Inflate (sbam_inflate.hip): entropy decode into per-block token regions (wave-parallel fast path, per-lane
 // exact path for the blocks it hands over), then LZ77 resolve into `out`.  tok: inflate_token_bytes(L, nb) bytes;
 // slow: nb int32; counters: 3 × u32 device scratch, reset by the decode launch.
@@ -155,8 +156,10 @@ hipError_t launch_record_offsets(StreamView sv, int64_t x0, int64_t x_end, int64
 // at x, xa 64-aligned.  fail: i32 device flag, set to 1 when the chain is not the bitmap's set bits.
 hipError_t launch_chain_proof(const uint8_t *u, int64_t L, const unsigned long long *bm, int64_t xa, int64_t X0,
                               int64_t X1, int32_t *fail, const unsigned long long *exact, hipStream_t s);
+// (list, nlist, exact: the chain pass's PASS0 list and counters when the bitmap came from it, else nullptr)
 hipError_t launch_split_popcounts(const unsigned long long *bm, int64_t xa, const int64_t *xs, const int64_t *xe,
-                                  int64_t n, int64_t *counts, int32_t *fail, hipStream_t s);
+                                  int64_t n, int64_t *counts, int32_t *fail, const int64_t *list, int64_t nlist,
+                                  const unsigned long long *exact, hipStream_t s);
 hipError_t launch_split_offsets(const unsigned long long *bm, int64_t xa, const int64_t *xs, const int64_t *xe,
                                 const int64_t *base, int64_t n, int64_t *out, hipStream_t s);
 hipError_t launch_record_walk(const uint8_t *u, int64_t L, const int64_t *xs, const int64_t *xe, const int64_t *base,
