@@ -291,3 +291,33 @@ def test_concurrent_handles_match_serial():
     for t in ts:
         t.join()
     assert not errors, errors
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["1.bam", "2.bam", "5k.bam"])
+def test_block_table_before_inflate_gpu(name):
+    """The fast scan leaves the block table's host copy in flight (pinned staging filled on a side stream; the host
+    picks it up on its first read, or while inflate's kernels run).  Read straight after the scan, after a second
+    scan whose predecessor's copy was never read, and for a shard whose first block is found by FindBlockStart, the
+    table equals the oracle's, and the stream inflated afterwards has the oracle's length."""
+    import numpy as np
+    import oracle
+    import sbam
+    from conftest import fixture_bytes
+    data = fixture_bytes(name)
+    o = oracle.BamFile(data)
+    want = (o.start, o.csize, o.usize, o.uoff[:-1])
+    with sbam.BamFile(data, inflate=False) as f:
+        assert all(np.array_equal(x, y) for x, y in zip(f.blocks(), want))
+        f.reset()
+        f.n_blocks = f._scan()
+        f.n_blocks = f._scan()
+        assert f.inflate() == o.L
+        assert all(np.array_equal(x, y) for x, y in zip(f.blocks(), want))
+    k0 = o.nblocks // 3
+    lo = int(o.start[k0]) - 7  # inside the previous block: the shard starts at block k0
+    with sbam.BamFile(data[lo:], base_offset=lo, file_size=len(data), inflate=False) as f:
+        st, cs, us, uo = f.blocks()
+        assert np.array_equal(st, o.start[k0:]) and np.array_equal(cs, o.csize[k0:])
+        assert np.array_equal(us, o.usize[k0:]) and np.array_equal(uo, o.uoff[k0:-1] - o.uoff[k0])
+        assert f.inflate() == o.L - int(o.uoff[k0])
