@@ -341,10 +341,14 @@ __global__ __launch_bounds__(256) void k_chains(StreamView sv, int64_t x0, int64
 // position.
 __global__ __launch_bounds__(256) void k_p0_count(const unsigned long long *__restrict__ bitmap, int64_t nwords,
                                                   int32_t *__restrict__ chunk_cnt) {
-  const int64_t w0 = (int64_t)blockIdx.x * kChainWords + (int64_t)threadIdx.x * kChainWordsPerThread;
+  // (coalesced: thread t counts words t + 256 j of the chunk — the order does not matter for a count)
+  const int64_t cb = (int64_t)blockIdx.x * kChainWords + threadIdx.x;
   uint32_t c = 0;
 #pragma unroll
-  for (int j = 0; j < kChainWordsPerThread; j++) c += w0 + j < nwords ? (uint32_t)__popcll(bitmap[w0 + j]) : 0u;
+  for (int j = 0; j < kChainWordsPerThread; j++) {
+    const int64_t w = cb + 256 * j;
+    c += w < nwords ? (uint32_t)__popcll(bitmap[w]) : 0u;
+  }
   c = wave_sum(c);
   __shared__ uint32_t s_c[4];
   if (lane_id() == 0) s_c[threadIdx.x >> 6] = c;
@@ -397,12 +401,26 @@ __global__ __launch_bounds__(1024) void k_p0_scan(const int32_t *__restrict__ cn
 __global__ __launch_bounds__(256) void k_p0_list(const unsigned long long *__restrict__ bitmap, int64_t nwords,
                                                  int64_t x0a, const int64_t *__restrict__ chunk_off,
                                                  int64_t *__restrict__ list) {
-  const int64_t w0 = (int64_t)blockIdx.x * kChainWords + (int64_t)threadIdx.x * kChainWordsPerThread;
+  // The chunk's words go through LDS: loaded coalesced (thread t loads words t + 256 j), read back as each thread's
+  // own run of 8 consecutive words (the list is written in position order, one run per thread); rows padded to 9
+  // words, so the read-back is 2-way bank-conflicted instead of 16-way.  (Each thread reading its 8 words straight
+  // from memory left every load instruction touching 32 lines for 512 useful bytes.)
+  static_assert(kChainWordsPerThread == 8, "k_p0_list: 8-word runs");
+  constexpr int kRow = kChainWordsPerThread + 1;
+  __shared__ unsigned long long s_cw[256 * kRow];
+  const int64_t cb = (int64_t)blockIdx.x * kChainWords;
+#pragma unroll
+  for (int j = 0; j < kChainWordsPerThread; j++) {
+    const int i = (int)threadIdx.x + 256 * j;  // the chunk's word i: thread i / 8's word i % 8
+    s_cw[(i >> 3) * kRow + (i & 7)] = cb + i < nwords ? bitmap[cb + i] : 0ull;
+  }
+  __syncthreads();
+  const int64_t w0 = cb + (int64_t)threadIdx.x * kChainWordsPerThread;
   unsigned long long cw[kChainWordsPerThread];
   uint32_t mine = 0;
 #pragma unroll
   for (int j = 0; j < kChainWordsPerThread; j++) {
-    cw[j] = w0 + j < nwords ? bitmap[w0 + j] : 0ull;
+    cw[j] = s_cw[threadIdx.x * kRow + j];
     mine += (uint32_t)__popcll(cw[j]);
   }
   const int lane = lane_id(), wv = threadIdx.x >> 6;
